@@ -1,0 +1,117 @@
+"""Seeded synthetic multi-view calibration scenes.
+
+Replaces the reference's random scene generator
+(``data/camera_and_parameters_dataset.py:48-151``, which does not parse in the
+reference snapshot) with a deterministic one: problem ``i`` of a batch is a
+pure function of ``(seed, i)``, so any contiguous shard of a batch can be
+generated on its own rank with no scatter.
+
+Distributions (per problem):
+
+* f = 1/tan(a/2), a ~ U(pi/6, 2pi/3)                 (dataset ``:148-150``)
+* cx, cy ~ clamp(0.2 N(0,1), -0.5, 0.5)               (``:149``)
+* X_xy ~ N(0, 3^2), X_z ~ |20 + 5 N(0,1)|             (``:90-94``)
+* t_m ~ N(0, 3^2), w_m ~ N(0, 0.3^2)                  (``:110``)
+* k1 ~ N(0, 1e-2^2), k2 ~ N(0, 1e-3^2), k3 ~ N(0, 1e-4^2), p1, p2 ~ N(0, 1e-3^2)
+* observations: noise-free projection of the truth (fp64, then fp32)
+* visibility: |u| < 1 and |v| < 1 (``:194-197``) or all-true (roofline runs)
+* initial guess x0 = truth + N(0, 0.01^2) on the pinhole block; the five
+  distortion coefficients get 10 % of their own spread
+  (N(0, [1e-3, 1e-4, 1e-5, 1e-4, 1e-4]^2)) -- a 0.01 kick on k3 (spread 1e-4)
+  is 100 sigma and sends k3 r^6 to ~1e2 at the image edge.
+
+Parameter layout: see ``camera_model.layout``.
+"""
+from typing import NamedTuple
+
+import numpy as np
+
+
+class SceneBatch(NamedTuple):
+    truth: np.ndarray  # (B, P) float64
+    initial: np.ndarray  # (B, P) float32
+    observations: np.ndarray  # (B, M, N, 2) float32
+    visibility: np.ndarray  # (B, M, N) bool
+    num_views: int
+    num_points: int
+    distortion: bool
+
+
+def parameter_count(num_views: int, num_points: int, distortion: bool) -> int:
+    return 3 + 3 * num_points + 6 * (num_views - 1) + (5 if distortion else 0)
+
+
+def _rotate(v: np.ndarray, w: np.ndarray) -> np.ndarray:
+    """Rodrigues in fp64, v (N,3), w (3,)."""
+    theta = np.linalg.norm(w)
+    if theta < 1e-12:
+        return v.copy()
+    k = w / theta
+    c, s = np.cos(theta), np.sin(theta)
+    return v * c + np.cross(k, v) * s + np.outer(v @ k, k) * (1.0 - c)
+
+
+def project_truth(x: np.ndarray, num_views: int, num_points: int, distortion: bool) -> np.ndarray:
+    """(M, N, 2) fp64 projection of one parameter vector (no scale normalisation:
+    the projection is invariant to it)."""
+    f, cx, cy = x[0], x[1], x[2]
+    pts = x[3:3 + 3 * num_points].reshape(num_points, 3)
+    base = 3 + 3 * num_points
+    ts = x[base:base + 3 * (num_views - 1)].reshape(num_views - 1, 3)
+    ws = x[base + 3 * (num_views - 1):base + 6 * (num_views - 1)].reshape(num_views - 1, 3)
+    out = np.empty((num_views, num_points, 2))
+    for m in range(num_views):
+        p = pts if m == 0 else _rotate(pts, ws[m - 1]) + ts[m - 1]
+        u = f * p[:, 0] / p[:, 2]
+        v = f * p[:, 1] / p[:, 2]
+        if distortion:
+            k1, k2, k3, p1, p2 = x[base + 6 * (num_views - 1):base + 6 * (num_views - 1) + 5]
+            r2 = u * u + v * v
+            radial = 1.0 + k1 * r2 + k2 * r2 * r2 + k3 * r2 * r2 * r2
+            u, v = (u * radial + 2.0 * p1 * u * v + p2 * (r2 + 2 * u * u),
+                    v * radial + 2.0 * p2 * u * v + p1 * (r2 + 2 * v * v))
+        out[m, :, 0] = u + cx
+        out[m, :, 1] = v + cy
+    return out
+
+
+def make_scenes(
+    batch: int,
+    num_views: int,
+    num_points: int,
+    distortion: bool = False,
+    seed: int = 20251015,
+    first_index: int = 0,
+    all_visible: bool = False,
+    initial_noise: float = 0.01,
+) -> SceneBatch:
+    """Problems ``first_index .. first_index + batch - 1`` of the stream ``seed``."""
+    if num_views < 2:
+        raise ValueError("num_views must be >= 2 (the scale normalisation needs a translation)")
+    p = parameter_count(num_views, num_points, distortion)
+    truth = np.empty((batch, p))
+    initial = np.empty((batch, p), dtype=np.float32)
+    obs = np.empty((batch, num_views, num_points, 2), dtype=np.float32)
+    vis = np.empty((batch, num_views, num_points), dtype=bool)
+    for b in range(batch):
+        rng = np.random.default_rng([seed, first_index + b])
+        a = np.pi / 6 + (np.pi / 2) * rng.random()
+        f = 1.0 / np.tan(a / 2.0)
+        c = np.clip(0.2 * rng.standard_normal(2), -0.5, 0.5)
+        xy = 3.0 * rng.standard_normal((num_points, 2))
+        z = np.abs(20.0 + 5.0 * rng.standard_normal((num_points, 1)))
+        t = 3.0 * rng.standard_normal((num_views - 1, 3))
+        w = 0.3 * rng.standard_normal((num_views - 1, 3))
+        row = [np.array([f, c[0], c[1]]), np.concatenate([xy, z], axis=1).ravel(), t.ravel(), w.ravel()]
+        if distortion:
+            row.append(rng.standard_normal(5) * np.array([1e-2, 1e-3, 1e-4, 1e-3, 1e-3]))
+        x = np.concatenate(row)
+        truth[b] = x
+        uv = project_truth(x, num_views, num_points, distortion)
+        obs[b] = uv
+        vis[b] = True if all_visible else (np.abs(uv[..., 0]) < 1.0) & (np.abs(uv[..., 1]) < 1.0)
+        kick = initial_noise * rng.standard_normal(p)
+        if distortion:
+            kick[-5:] *= np.array([1e-1, 1e-2, 1e-3, 1e-2, 1e-2])
+        initial[b] = x + kick
+    return SceneBatch(truth, initial, obs, vis, num_views, num_points, distortion)

@@ -1,0 +1,214 @@
+"""Generate golden vectors from the REAL reference (build container only).
+
+Run:   python tests/golden/make_golden.py          (needs /root/reference)
+
+The reference (jskinn/deep-attention-visual-odometry @ 2025-04-04) is
+imported from /root/reference; only its OUTPUTS are committed, as small
+``.npz`` fixtures next to this script.  Nothing here travels to the GPU box
+except those fixtures.
+
+Import note: ``camera_model/__init__.py`` pulls in modules that use
+``typing.Self`` (Python >= 3.11); this container has 3.10, so the ordinary
+ImportError is avoided by aliasing ``typing_extensions.Self`` in THIS
+process before the import (the survey did the same).  The
+reference files are untouched.
+
+Fixtures written:
+
+* ``ba_eval.npz``     -- reprojection error + autograd gradient of the
+                          reference-composed objective (unpack ->
+                          get_camera_relative_points -> rotate_vector_axis_angle
+                          -> project_points_basic_pinhole -> squared residual),
+                          fp64 and fp32, for the C1/C2/C3 shapes at B = 1.
+* ``bfgs_update.npz`` -- ``BFGSSolver.update_inverse_hessian`` and
+                          ``scale_initial_inverse_hessian`` on random inputs.
+* ``line_search.npz`` -- ``line_search_wolfe_conditions`` alphas (strong and
+                          weak) on BA objectives along the negative gradient.
+* ``bfgs_traj.npz``   -- ``BFGSSolver(...).eval()`` results after K in
+                          {5, 20, 100} iterations (error_threshold = -1,
+                          minimum_step = -1) for C1 (2x64), C2 (2x128) and
+                          C3-pinhole (4x256) shapes, plus one run with the
+                          reference's default thresholds.
+"""
+import os
+import sys
+import typing
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, "deep-attention-visual-odometry_amd"))
+sys.path.insert(0, "/root/reference")
+
+import typing_extensions  # noqa: E402
+
+if not hasattr(typing, "Self"):
+    typing.Self = typing_extensions.Self
+
+from deep_attention_visual_odometry.autograd_solvers import BFGSSolver  # noqa: E402
+from deep_attention_visual_odometry.autograd_solvers.line_search import line_search_wolfe_conditions  # noqa: E402
+from deep_attention_visual_odometry.camera_model import (  # noqa: E402
+    get_camera_relative_points,
+    unpack_calibration_parameters,
+)
+from deep_attention_visual_odometry.geometry import (  # noqa: E402
+    project_points_basic_pinhole,
+    rotate_vector_axis_angle,
+)
+
+from deep_attention_visual_odometry_amd.scenes import make_scenes  # noqa: E402
+
+SHAPES = {"c1": (2, 64), "c2": (2, 128), "c3": (4, 256)}
+
+
+def ref_relative_points(points, translations, rotations, batch):
+    """The reference's own function at B=1; at B>1 the same composition with the
+    scale kept broadcastable (the reference's version mis-broadcasts for B>1,
+    SURVEY.md 0.5), still using the reference's rotate_vector_axis_angle."""
+    if batch == 1:
+        return get_camera_relative_points(points, translations, rotations)
+    n = points.size(-2)
+    m = translations.size(-3) + 1
+    ps = points.abs().mean(dim=(-1, -2, -3), keepdim=True)
+    cs = translations.abs().mean(dim=(-1, -2, -3), keepdim=True)
+    s = (ps * n + cs * m) / (n + m)
+    translations = translations / s
+    points = points / s
+    moved = rotate_vector_axis_angle(points, rotations) + translations
+    return torch.concatenate([points, moved], dim=-3)
+
+
+def ref_objective(x, obs, vis, m, n):
+    parts = unpack_calibration_parameters(x, m, n)
+    rel = ref_relative_points(parts.world_points, parts.camera_translations, parts.camera_rotations, x.shape[0])
+    uv = project_points_basic_pinhole(rel, parts.intrinsics)
+    sq = (uv - obs).square().sum(dim=-1)
+    return (sq * vis.to(sq.dtype)).sum(dim=(-1, -2))
+
+
+def closure_for(obs, vis, m, n, batch_mask_full=None):
+    def fn(x, mask):
+        # x is (K, P) with K == mask.sum(); a single-problem batch keeps B == 1
+        return ref_objective(x, obs[mask], vis[mask], m, n)
+
+    return fn
+
+
+def scenes_as_tensors(batch, m, n, seed, dtype):
+    s = make_scenes(batch, m, n, distortion=False, seed=seed)
+    return (
+        s,
+        torch.tensor(s.initial, dtype=dtype),
+        torch.tensor(s.observations, dtype=dtype),
+        torch.tensor(s.visibility),
+    )
+
+
+def gen_ba_eval():
+    out = {}
+    for name, (m, n) in SHAPES.items():
+        for dt_name, dt in (("f64", torch.float64), ("f32", torch.float32)):
+            s, x0, obs, vis = scenes_as_tensors(1, m, n, 7001, dt)
+            x = x0.clone().requires_grad_(True)
+            e = ref_objective(x, obs, vis, m, n)
+            (g,) = torch.autograd.grad(e.sum(), x)
+            key = f"{name}_{dt_name}"
+            out[key + "_x"] = x0.numpy()
+            out[key + "_obs"] = obs.numpy()
+            out[key + "_vis"] = vis.numpy()
+            out[key + "_err"] = e.detach().numpy()
+            out[key + "_grad"] = g.numpy()
+    np.savez_compressed(os.path.join(HERE, "ba_eval.npz"), **out)
+
+
+def gen_bfgs_update():
+    out = {}
+    rng = np.random.default_rng(424242)
+    for dt_name, dt in (("f64", torch.float64), ("f32", torch.float32)):
+        for p in (3, 17, 64):
+            k = 4
+            a = rng.normal(size=(k, p, p))
+            h = torch.tensor(a @ a.transpose(0, 2, 1) / p + np.eye(p), dtype=dt)
+            s = torch.tensor(rng.normal(size=(k, p)), dtype=dt)
+            y = torch.tensor(rng.normal(size=(k, p)), dtype=dt)
+            y[1] = -s[1]  # negative curvature -> update skipped
+            key = f"{dt_name}_p{p}"
+            out[key + "_h"] = h.numpy()
+            out[key + "_s"] = s.numpy()
+            out[key + "_y"] = y.numpy()
+            out[key + "_out"] = BFGSSolver.update_inverse_hessian(h, s, y).numpy()
+            out[key + "_scale"] = BFGSSolver.scale_initial_inverse_hessian(s, y).numpy()
+    np.savez_compressed(os.path.join(HERE, "bfgs_update.npz"), **out)
+
+
+def gen_line_search():
+    out = {}
+    for name, (m, n) in SHAPES.items():
+        for dt_name, dt in (("f64", torch.float64), ("f32", torch.float32)):
+            batch = 4
+            s, x0, obs, vis = scenes_as_tensors(batch, m, n, 7100, dt)
+            x = x0.clone().requires_grad_(True)
+            e = ref_objective(x, obs, vis, m, n)
+            (g,) = torch.autograd.grad(e.sum(), x)
+            d = -g
+            # problem 2 searches uphill: alpha -> 0 (pinned by the reference tests)
+            d[2] = g[2]
+            fn = closure_for(obs, vis, m, n)
+            for strong in (True, False):
+                alpha = line_search_wolfe_conditions(x0, d, e.detach(), g, fn, strong=strong)
+                out[f"{name}_{dt_name}_{'strong' if strong else 'weak'}_alpha"] = alpha.numpy()
+            key = f"{name}_{dt_name}"
+            out[key + "_x"] = x0.numpy()
+            out[key + "_obs"] = obs.numpy()
+            out[key + "_vis"] = vis.numpy()
+            out[key + "_dir"] = d.numpy()
+            out[key + "_err"] = e.detach().numpy()
+            out[key + "_grad"] = g.numpy()
+    np.savez_compressed(os.path.join(HERE, "line_search.npz"), **out)
+
+
+def gen_trajectories():
+    out = {}
+    cases = [
+        ("c1", 4, (5, 20, 100)),
+        ("c2", 2, (5, 20, 100)),
+        ("c3", 2, (5, 20)),
+    ]
+    for name, batch, ks in cases:
+        m, n = SHAPES[name]
+        s, x0, obs, vis = scenes_as_tensors(batch, m, n, 7200, torch.float32)
+        key = name
+        out[key + "_x0"] = x0.numpy()
+        out[key + "_obs"] = obs.numpy()
+        out[key + "_vis"] = vis.numpy()
+        out[key + "_truth"] = s.truth
+        for k in ks:
+            solver = BFGSSolver(iterations=k, error_threshold=-1.0, minimum_step=-1.0).eval()
+            xk = solver(x0, closure_for(obs, vis, m, n))
+            out[f"{key}_k{k}"] = xk.numpy()
+    # reference defaults, run to the stopping rules (one C1 problem, fp64)
+    m, n = SHAPES["c1"]
+    s, x0, obs, vis = scenes_as_tensors(1, m, n, 7300, torch.float64)
+    solver = BFGSSolver().eval()
+    out["c1def_x0"] = x0.numpy()
+    out["c1def_obs"] = obs.numpy()
+    out["c1def_vis"] = vis.numpy()
+    out["c1def_out"] = solver(x0, closure_for(obs, vis, m, n)).numpy()
+    np.savez_compressed(os.path.join(HERE, "bfgs_traj.npz"), **out)
+
+
+if __name__ == "__main__":
+    torch.set_num_threads(8)
+    which = sys.argv[1:] or ["eval", "update", "ls", "traj"]
+    if "eval" in which:
+        gen_ba_eval()
+    if "update" in which:
+        gen_bfgs_update()
+    if "ls" in which:
+        gen_line_search()
+    if "traj" in which:
+        gen_trajectories()
+    print("golden fixtures written to", HERE)
