@@ -1,0 +1,401 @@
+// Multi-view pinhole (+ Brown-Conrady) squared reprojection objective on gfx950.
+//
+// E(x) = sum_{m,n} vis[m,n] * || pi_m(X_n) - obs[m,n] ||^2      
+//
+// One problem per 256-thread workgroup.  Threads own points (n = tid, tid+256,
+// ...); each thread sweeps every view for its points, so a point's gradient
+// never needs a cross-thread reduction.  Per-view gradients (translation,
+// rotation) are wave-reduced per view and summed across the 4 waves once, and
+// the intrinsics / scale-path sums go through one deterministic block
+// reduction.  Three flavours share the code:
+//   GRAD  : reverse mode, writes dE/dx into an LDS vector (replaces
+//           torch.autograd.grad in bfgs_solver.py:133-135),
+//   SLOPE : forward mode along a direction d, returns phi'(alpha) = d . grad E
+//           (replaces the autograd-w.r.t.-alpha trick of wolfe_conditions.py:134-143),
+//   TRIAL : evaluate at x + alpha*d formed on the fly, rounded exactly as the
+//           reference forms `parameters + alpha * direction`.
+// Forward-model references:
+//   scale normalisation   camera_model/calibration_pinhole_camera_model.py:97-104
+//   Rodrigues             geometry/axis_angle_rotation.py:25-48
+//   Taylor branches       utils/func_sin_x_on_x.py:5-98, utils/func_one_minus_cos_x_on_x_squared.py:6-51
+//   pinhole               geometry/camera_projection.py:20-35
+//   Brown-Conrady         camera_model/distorted_camera_model.py:59-86 (fx = fy = f, s = 0)
+// Derivatives are derived here by hand (the reference's analytic BC Jacobian is
+// wrong) and checked against autograd of the oracle in tests/.
+#pragma once
+
+#include "dava_common.hpp"
+
+namespace dava {
+
+struct Layout {
+  int M, N, P, distort;
+  __device__ __forceinline__ int pt(int n) const { return 3 + 3 * n; }
+  __device__ __forceinline__ int tr(int m) const { return 3 + 3 * N + 3 * (m - 1); }
+  __device__ __forceinline__ int rot(int m) const { return 3 + 3 * N + 3 * (M - 1) + 3 * (m - 1); }
+  __device__ __forceinline__ int dist() const { return 3 + 3 * N + 6 * (M - 1); }
+};
+
+// ---- Taylor-branched ratios, same thresholds and series as the reference ----
+__device__ __forceinline__ float sinc(float x) {
+  if (fabsf(x) < 0.01f) {
+    const float x2 = x * x, x4 = x2 * x2, x6 = x4 * x2;
+    return 1.0f - x2 / 6.0f + x4 / 120.0f - x6 / 5040.0f;
+  }
+  return sinf(x) / x;
+}
+__device__ __forceinline__ float sinc_slope(float x) {  // cos/x^2 - sin/x^3
+  const float x2 = x * x;
+  if (fabsf(x) < 0.01f) {
+    const float x4 = x2 * x2, x6 = x4 * x2;
+    return -1.0f / 3.0f + x2 / 30.0f - x4 / 840.0f + x6 / 45360.0f;
+  }
+  return cosf(x) / x2 - sinf(x) / (x * x2);
+}
+__device__ __forceinline__ float versine_ratio(float x) {  // (1 - cos x)/x^2
+  const float x2 = x * x;
+  if (fabsf(x) < 0.05f) {
+    const float x4 = x2 * x2, x6 = x4 * x2;
+    return 0.5f - x2 / 24.0f + x4 / 720.0f - x6 / 40320.0f;
+  }
+  return (1.0f - cosf(x)) / x2;
+}
+
+// ---- per-view constants, kept in LDS (one row of kViewStride floats per view >= 1) ----
+constexpr int kViewStride = 24;
+enum ViewField {
+  VW0 = 0, VW1, VW2,     // rotation (trial value)
+  VCOS, VA, VB, VSIN,    // cos th, (1-cos)/th^2, sin/th, sin th
+  VRCP, VAP, VTC,        // 1/th (0 at 0), dA/dth, dB/dth
+  VDW0, VDW1, VDW2, VDTH,// direction of w, d th
+  VT0, VT1, VT2,         // translation (trial value, unnormalised)
+  VDT0, VDT1, VDT2       // direction of t
+};
+
+// Partial sums per view kept by each wave: 8 floats {gw_direct xyz, g_theta, g_t~ xyz, -}
+constexpr int kViewPart = 8;
+
+// LDS footprint helpers (floats)
+__host__ __device__ inline int views_floats(int M) { return (M - 1) * kViewStride; }
+__host__ __device__ inline int vpart_floats(int M) { return M * kWaves * kViewPart; }
+
+struct Intrinsics {
+  float f, cx, cy, k1, k2, k3, p1, p2;
+};
+
+template <bool TRIAL>
+__device__ __forceinline__ float trial_value(const float* x, const float* d, float a, int i) {
+  if constexpr (TRIAL) return __fadd_rn(x[i], __fmul_rn(a, d[i]));
+  else return x[i];
+}
+
+// Evaluate E (and optionally its gradient and/or slope along d) for one problem.
+// All 256 threads must call; E / slope come back identical in every thread.
+//   x, d, grad, obs, vis, views, vpart, scratch : LDS
+//   buf : reduction double-buffer toggle (updated)
+template <bool GRAD, bool SLOPE, bool TRIAL>
+__device__ void ba_eval(const Layout& L, const float* x, const float* d, float alpha, const float* obs,
+                        const uint8_t* vis, float* grad, float* views, float* vpart, float* scratch, int& buf,
+                        float& E_out, float& slope_out) {
+  const int tid = threadIdx.x;
+  const int lane = tid & (kWave - 1);
+  const int wave = tid / kWave;
+  const int M = L.M, N = L.N;
+
+  // 1. per-view rotation constants (views 1..M-1), one thread per view
+  for (int m = 1 + tid; m < M; m += kBlock) {
+    float* v = views + (m - 1) * kViewStride;
+    const int r = L.rot(m), t = L.tr(m);
+    const float w0 = trial_value<TRIAL>(x, d, alpha, r + 0);
+    const float w1 = trial_value<TRIAL>(x, d, alpha, r + 1);
+    const float w2 = trial_value<TRIAL>(x, d, alpha, r + 2);
+    const float th = sqrtf(w0 * w0 + w1 * w1 + w2 * w2);
+    const float A = versine_ratio(th), B = sinc(th);
+    const float rcp = th == 0.0f ? 0.0f : 1.0f / th;
+    v[VW0] = w0; v[VW1] = w1; v[VW2] = w2;
+    v[VCOS] = cosf(th); v[VA] = A; v[VB] = B; v[VSIN] = sinf(th);
+    v[VRCP] = rcp;
+    v[VAP] = rcp * (B - 2.0f * A);       // d/dth (1-cos)/th^2, reference backward form
+    v[VTC] = th * sinc_slope(th);        // d/dth sin(th)/th
+    v[VT0] = trial_value<TRIAL>(x, d, alpha, t + 0);
+    v[VT1] = trial_value<TRIAL>(x, d, alpha, t + 1);
+    v[VT2] = trial_value<TRIAL>(x, d, alpha, t + 2);
+    if constexpr (SLOPE) {
+      const float d0 = d[r], d1 = d[r + 1], d2 = d[r + 2];
+      v[VDW0] = d0; v[VDW1] = d1; v[VDW2] = d2;
+      v[VDTH] = (w0 * d0 + w1 * d1 + w2 * d2) * rcp;
+      v[VDT0] = d[t]; v[VDT1] = d[t + 1]; v[VDT2] = d[t + 2];
+    }
+  }
+
+  // 2. scale normalisation s = (mean|X| N + mean|t| M)/(N+M), and its slope
+  float sums[2] = {0.f, 0.f};
+  for (int n = tid; n < N; n += kBlock) {
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      const float X = trial_value<TRIAL>(x, d, alpha, L.pt(n) + c);
+      sums[0] += fabsf(X);
+      if constexpr (SLOPE) sums[1] += sgn(X) * d[L.pt(n) + c];
+    }
+  }
+  if constexpr (SLOPE) block_sum<2>(sums, scratch, buf);
+  else block_sum<1>(reinterpret_cast<float(&)[1]>(sums), scratch, buf);
+  buf ^= 1;  // (this barrier also publishes the view constants)
+  float tsum = 0.f, tdsum = 0.f;
+  for (int i = L.tr(1); i < L.tr(1) + 3 * (M - 1); ++i) {
+    const float t = trial_value<TRIAL>(x, d, alpha, i);
+    tsum += fabsf(t);
+    if constexpr (SLOPE) tdsum += sgn(t) * d[i];
+  }
+  const float fN = (float)N, fM = (float)M, fNM = (float)(N + M);
+  const float ps = sums[0] / (3.0f * fN);
+  const float cs = tsum / (3.0f * (float)(M - 1));
+  const float s = (ps * fN + cs * fM) / fNM;
+  const float inv_s = 1.0f / s;
+  float ds_over_s = 0.f;
+  if constexpr (SLOPE) {
+    const float ds = ((sums[1] / (3.0f * fN)) * fN + (tdsum / (3.0f * (float)(M - 1))) * fM) / fNM;
+    ds_over_s = ds * inv_s;
+  }
+
+  // 3. intrinsics (trial values + directions)
+  Intrinsics in, din;
+  in.f = trial_value<TRIAL>(x, d, alpha, 0);
+  in.cx = trial_value<TRIAL>(x, d, alpha, 1);
+  in.cy = trial_value<TRIAL>(x, d, alpha, 2);
+  in.k1 = in.k2 = in.k3 = in.p1 = in.p2 = 0.f;
+  din = Intrinsics{0, 0, 0, 0, 0, 0, 0, 0};
+  const int kd = L.dist();
+  if (L.distort) {
+    in.k1 = trial_value<TRIAL>(x, d, alpha, kd + 0);
+    in.k2 = trial_value<TRIAL>(x, d, alpha, kd + 1);
+    in.k3 = trial_value<TRIAL>(x, d, alpha, kd + 2);
+    in.p1 = trial_value<TRIAL>(x, d, alpha, kd + 3);
+    in.p2 = trial_value<TRIAL>(x, d, alpha, kd + 4);
+  }
+  if constexpr (SLOPE) {
+    din.f = d[0]; din.cx = d[1]; din.cy = d[2];
+    if (L.distort) { din.k1 = d[kd]; din.k2 = d[kd + 1]; din.k3 = d[kd + 2]; din.p1 = d[kd + 3]; din.p2 = d[kd + 4]; }
+  }
+
+  float e_loc = 0.f, sl_loc = 0.f;
+  float gin[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // f cx cy k1 k2 k3 p1 p2
+  float gsx = 0.f;                          // sum gX~ . X  (scale path)
+
+  // 4. sweep views (outer) x own points (inner)
+  for (int m = 0; m < M; ++m) {
+    const float* v = views + (m > 0 ? (m - 1) * kViewStride : 0);
+    float vc = 1.f, vA = 0.f, vB = 0.f, vs = 0.f, vAp = 0.f, vTC = 0.f;
+    float w0 = 0.f, w1 = 0.f, w2 = 0.f, tt0 = 0.f, tt1 = 0.f, tt2 = 0.f;
+    float dw0 = 0.f, dw1 = 0.f, dw2 = 0.f, dth = 0.f, dtt0 = 0.f, dtt1 = 0.f, dtt2 = 0.f;
+    if (m > 0) {
+      w0 = v[VW0]; w1 = v[VW1]; w2 = v[VW2];
+      vc = v[VCOS]; vA = v[VA]; vB = v[VB]; vs = v[VSIN]; vAp = v[VAP]; vTC = v[VTC];
+      tt0 = v[VT0] * inv_s; tt1 = v[VT1] * inv_s; tt2 = v[VT2] * inv_s;  // t~ = t / s
+      if constexpr (SLOPE) {
+        dw0 = v[VDW0]; dw1 = v[VDW1]; dw2 = v[VDW2]; dth = v[VDTH];
+        dtt0 = (v[VDT0] - tt0 * (ds_over_s * s)) * inv_s;
+        dtt1 = (v[VDT1] - tt1 * (ds_over_s * s)) * inv_s;
+        dtt2 = (v[VDT2] - tt2 * (ds_over_s * s)) * inv_s;
+      }
+    }
+    float vg[7] = {0, 0, 0, 0, 0, 0, 0};  // gw_direct xyz, g_theta, g_t~ xyz
+
+    for (int n = tid; n < N; n += kBlock) {
+      const int ip = L.pt(n);
+      const float X0 = trial_value<TRIAL>(x, d, alpha, ip + 0);
+      const float X1 = trial_value<TRIAL>(x, d, alpha, ip + 1);
+      const float X2 = trial_value<TRIAL>(x, d, alpha, ip + 2);
+      const float a0 = X0 * inv_s, a1 = X1 * inv_s, a2 = X2 * inv_s;  // X~ = X / s
+      float da0 = 0.f, da1 = 0.f, da2 = 0.f;
+      if constexpr (SLOPE) {
+        da0 = (d[ip + 0] - a0 * (ds_over_s * s)) * inv_s;
+        da1 = (d[ip + 1] - a1 * (ds_over_s * s)) * inv_s;
+        da2 = (d[ip + 2] - a2 * (ds_over_s * s)) * inv_s;
+      }
+      // camera-relative point p (and dp)
+      float p0, p1, p2, dp0 = 0.f, dp1 = 0.f, dp2 = 0.f;
+      float vw = 0.f, c0 = 0.f, c1 = 0.f, c2 = 0.f;  // v.w and w x v
+      if (m == 0) {
+        p0 = a0; p1 = a1; p2 = a2;
+        if constexpr (SLOPE) { dp0 = da0; dp1 = da1; dp2 = da2; }
+      } else {
+        vw = a0 * w0 + a1 * w1 + a2 * w2;
+        c0 = w1 * a2 - w2 * a1;
+        c1 = w2 * a0 - w0 * a2;
+        c2 = w0 * a1 - w1 * a0;
+        const float Avw = vA * vw;
+        p0 = a0 * vc + Avw * w0 + c0 * vB + tt0;
+        p1 = a1 * vc + Avw * w1 + c1 * vB + tt1;
+        p2 = a2 * vc + Avw * w2 + c2 * vB + tt2;
+        if constexpr (SLOPE) {
+          const float dc = -vs * dth, dA = vAp * dth, dB = vTC * dth;
+          const float dvw = (da0 * w0 + da1 * w1 + da2 * w2) + (a0 * dw0 + a1 * dw1 + a2 * dw2);
+          const float e0 = (dw1 * a2 - dw2 * a1) + (w1 * da2 - w2 * da1);
+          const float e1 = (dw2 * a0 - dw0 * a2) + (w2 * da0 - w0 * da2);
+          const float e2 = (dw0 * a1 - dw1 * a0) + (w0 * da1 - w1 * da0);
+          const float k = dA * vw + vA * dvw;
+          dp0 = da0 * vc + a0 * dc + k * w0 + Avw * dw0 + e0 * vB + c0 * dB + dtt0;
+          dp1 = da1 * vc + a1 * dc + k * w1 + Avw * dw1 + e1 * vB + c1 * dB + dtt1;
+          dp2 = da2 * vc + a2 * dc + k * w2 + Avw * dw2 + e2 * vB + c2 * dB + dtt2;
+        }
+      }
+      // projection
+      const float iz = 1.0f / p2;
+      const float qx = p0 * iz, qy = p1 * iz;
+      const float ub = in.f * qx, vb = in.f * qy;
+      float u, vv, dub = 0.f, dvb = 0.f;
+      float Juu = 1.f, Juv = 0.f, Jvv = 1.f, r2 = 0.f;
+      if constexpr (SLOPE) {
+        const float dqx = (dp0 - qx * dp2) * iz, dqy = (dp1 - qy * dp2) * iz;
+        dub = din.f * qx + in.f * dqx;
+        dvb = din.f * qy + in.f * dqy;
+      }
+      if (L.distort) {
+        r2 = ub * ub + vb * vb;
+        const float D = 1.0f + in.k1 * r2 + in.k2 * r2 * r2 + in.k3 * r2 * r2 * r2;
+        const float Dr = in.k1 + 2.0f * in.k2 * r2 + 3.0f * in.k3 * r2 * r2;
+        const float uvb = ub * vb;
+        u = ub * D + 2.0f * in.p1 * uvb + in.p2 * (r2 + 2.0f * ub * ub) + in.cx;
+        vv = vb * D + 2.0f * in.p2 * uvb + in.p1 * (r2 + 2.0f * vb * vb) + in.cy;
+        Juu = D + 2.0f * ub * ub * Dr + 2.0f * in.p1 * vb + 6.0f * in.p2 * ub;
+        Juv = 2.0f * uvb * Dr + 2.0f * in.p1 * ub + 2.0f * in.p2 * vb;
+        Jvv = D + 2.0f * vb * vb * Dr + 2.0f * in.p2 * ub + 6.0f * in.p1 * vb;
+      } else {
+        u = ub + in.cx;
+        vv = vb + in.cy;
+      }
+      const int pair = m * N + n;
+      const float wgt = (float)vis[pair];
+      const float ru = u - obs[2 * pair], rv = vv - obs[2 * pair + 1];
+      e_loc += (ru * ru + rv * rv) * wgt;
+      if constexpr (SLOPE) {
+        float du = Juu * dub + Juv * dvb + din.cx;
+        float dv = Juv * dub + Jvv * dvb + din.cy;
+        if (L.distort) {
+          const float r4 = r2 * r2;
+          du += ub * (r2 * din.k1 + r4 * din.k2 + r4 * r2 * din.k3) + 2.0f * ub * vb * din.p1 +
+                (r2 + 2.0f * ub * ub) * din.p2;
+          dv += vb * (r2 * din.k1 + r4 * din.k2 + r4 * r2 * din.k3) + (r2 + 2.0f * vb * vb) * din.p1 +
+                2.0f * ub * vb * din.p2;
+        }
+        sl_loc += 2.0f * wgt * (ru * du + rv * dv);
+      }
+      if constexpr (GRAD) {
+        const float gu = 2.0f * wgt * ru, gv = 2.0f * wgt * rv;
+        gin[1] += gu;
+        gin[2] += gv;
+        float gub = gu, gvb = gv;
+        if (L.distort) {
+          gub = gu * Juu + gv * Juv;
+          gvb = gu * Juv + gv * Jvv;
+          const float r4 = r2 * r2;
+          const float gr = gu * ub + gv * vb;
+          gin[3] += gr * r2;
+          gin[4] += gr * r4;
+          gin[5] += gr * r4 * r2;
+          gin[6] += gu * 2.0f * ub * vb + gv * (r2 + 2.0f * vb * vb);
+          gin[7] += gu * (r2 + 2.0f * ub * ub) + gv * 2.0f * ub * vb;
+        }
+        gin[0] += gub * qx + gvb * qy;
+        const float fi = in.f * iz;
+        const float G0 = gub * fi, G1 = gvb * fi, G2 = -(gub * ub + gvb * vb) * iz;
+        float gx0, gx1, gx2;
+        if (m == 0) {
+          gx0 = G0; gx1 = G1; gx2 = G2;
+        } else {
+          const float Gw = G0 * w0 + G1 * w1 + G2 * w2;
+          const float Gv = G0 * a0 + G1 * a1 + G2 * a2;
+          const float Gx = G0 * c0 + G1 * c1 + G2 * c2;
+          const float AGw = vA * Gw, Avw = vA * vw;
+          // dE/dX~ = c G + A (G.w) w + B (G x w)
+          gx0 = vc * G0 + AGw * w0 + vB * (G1 * w2 - G2 * w1);
+          gx1 = vc * G1 + AGw * w1 + vB * (G2 * w0 - G0 * w2);
+          gx2 = vc * G2 + AGw * w2 + vB * (G0 * w1 - G1 * w0);
+          // dE/dw (direct) = A vw G + A (G.w) X~ + B (X~ x G)
+          vg[0] += Avw * G0 + AGw * a0 + vB * (a1 * G2 - a2 * G1);
+          vg[1] += Avw * G1 + AGw * a1 + vB * (a2 * G0 - a0 * G2);
+          vg[2] += Avw * G2 + AGw * a2 + vB * (a0 * G1 - a1 * G0);
+          vg[3] += -vs * Gv + vAp * vw * Gw + vTC * Gx;  // dE/dth
+          vg[4] += G0; vg[5] += G1; vg[6] += G2;          // dE/dt~
+        }
+        float* gp = grad + ip;
+        if (m == 0) { gp[0] = gx0; gp[1] = gx1; gp[2] = gx2; }
+        else { gp[0] += gx0; gp[1] += gx1; gp[2] += gx2; }
+        if (m == M - 1) gsx += gp[0] * X0 + gp[1] * X1 + gp[2] * X2;
+      }
+    }
+    if constexpr (GRAD) {
+      if (m > 0) {
+#pragma unroll
+        for (int k = 0; k < 7; ++k) {
+          const float w = wave_sum(vg[k]);
+          if (lane == 0) vpart[(m * kWaves + wave) * kViewPart + k] = w;
+        }
+      }
+    }
+  }
+
+  // 5. block reduction of error, slope, intrinsics gradient and scale-path sum
+  if constexpr (GRAD) {
+    float r[11] = {e_loc, sl_loc, gin[0], gin[1], gin[2], gin[3], gin[4], gin[5], gin[6], gin[7], gsx};
+    block_sum<11>(r, scratch, buf);
+    buf ^= 1;
+    E_out = r[0];
+    slope_out = r[1];
+    // scale path: s = (ps N + cs M)/(N+M); X~ = X/s, t~ = t/s
+    float gst = 0.f;  // sum g_t~ . t
+    for (int m = 1; m < M; ++m) {
+      const float* v = views + (m - 1) * kViewStride;
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        const float* q = vpart + (m * kWaves) * kViewPart + 4 + c;
+        const float g = ((q[0] + q[kViewPart]) + q[2 * kViewPart]) + q[3 * kViewPart];
+        gst += g * v[VT0 + c];
+      }
+    }
+    const float gs = -(r[10] + gst) * inv_s * inv_s;
+    const float g_ps = gs * fN / fNM, g_cs = gs * fM / fNM;
+    const float gabsX = g_ps / (3.0f * fN);
+    const float gabsT = g_cs / (3.0f * (float)(M - 1));
+    for (int n = tid; n < N; n += kBlock) {
+      float* gp = grad + L.pt(n);
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        const float X = trial_value<TRIAL>(x, d, alpha, L.pt(n) + c);
+        gp[c] = gp[c] * inv_s + sgn(X) * gabsX;
+      }
+    }
+    for (int q = tid; q < 6 * (M - 1); q += kBlock) {
+      const int m = 1 + q / 6, c = q % 6;
+      const float* v = views + (m - 1) * kViewStride;
+      auto vsum = [&](int k) {
+        const float* p = vpart + (m * kWaves) * kViewPart + k;
+        return ((p[0] + p[kViewPart]) + p[2 * kViewPart]) + p[3 * kViewPart];
+      };
+      if (c < 3) {
+        grad[L.tr(m) + c] = vsum(4 + c) * inv_s + sgn(v[VT0 + c]) * gabsT;
+      } else {
+        const int k = c - 3;
+        grad[L.rot(m) + k] = vsum(k) + vsum(3) * v[VRCP] * v[VW0 + k];
+      }
+    }
+    if (tid == 0) {
+      grad[0] = r[2]; grad[1] = r[3]; grad[2] = r[4];
+      if (L.distort) {
+#pragma unroll
+        for (int k = 0; k < 5; ++k) grad[kd + k] = r[5 + k];
+      }
+    }
+    __syncthreads();
+  } else {
+    float r[2] = {e_loc, sl_loc};
+    if constexpr (SLOPE) block_sum<2>(r, scratch, buf);
+    else block_sum<1>(reinterpret_cast<float(&)[1]>(r), scratch, buf);
+    buf ^= 1;
+    E_out = r[0];
+    slope_out = r[1];
+  }
+}
+
+}  // namespace dava

@@ -1,0 +1,53 @@
+// Shared device helpers for the gfx950 BA solver (wave64, 256-thread workgroups).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "dava_ba.h"
+
+namespace dava {
+
+constexpr int kWave = 64;        // CDNA wavefront width
+constexpr int kBlock = 256;      // one problem per 256-thread workgroup (4 waves)
+constexpr int kWaves = kBlock / kWave;
+
+__host__ __device__ inline int round_up(int v, int m) { return (v + m - 1) / m * m; }
+
+// torch.clamp(min=lo) semantics: NaN propagates (fmaxf would swallow it).
+template <typename T>
+__device__ __forceinline__ T clamp_min(T v, T lo) { return v < lo ? lo : v; }
+
+// sign() as torch.abs backward uses it: 0 at 0.
+__device__ __forceinline__ float sgn(float v) { return v > 0.f ? 1.f : (v < 0.f ? -1.f : 0.f); }
+
+template <typename T>
+__device__ __forceinline__ T wave_sum(T v) {
+#pragma unroll
+  for (int off = kWave / 2; off > 0; off >>= 1) v += __shfl_xor(v, off, kWave);
+  return v;
+}
+
+// Deterministic block-wide sum of R values: wave butterflies, then the 4 wave
+// partials are added in a fixed order by every thread, so all threads hold
+// bit-identical results (the solver's control flow depends on them being
+// uniform).  `scratch` is double-buffered by the caller (alternate `buf`),
+// so ONE barrier per reduction suffices: a wave cannot reach the next use of
+// the same buffer before every wave has passed the intervening reduction's
+// barrier, i.e. before every wave finished reading this one.
+template <int R>
+__device__ __forceinline__ void block_sum(float (&v)[R], float* scratch, int buf) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wave = threadIdx.x / kWave;
+  float* s = scratch + buf * (kWaves * 32);
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    float w = wave_sum(v[r]);
+    if (lane == 0) s[wave * 32 + r] = w;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < R; ++r) v[r] = ((s[r] + s[32 + r]) + s[64 + r]) + s[96 + r];
+}
+
+}  // namespace dava

@@ -1,0 +1,19 @@
+"""MI355X-native batched BFGS bundle-adjustment solver.
+
+Drop-in for the hot path of jskinn/deep-attention-visual-odometry
+(``autograd_solvers/`` BFGS + strong-Wolfe on the ``camera_model/`` +
+``geometry/`` reprojection objective).  Compute runs in the gfx950 library
+``_lib/libdava_ba.so`` (C ABI: include/dava_ba.h); there is no CPU path.
+"""
+from .autograd_solvers import BFGSSolver, line_search_wolfe_conditions
+from .camera_model import ReprojectionError, num_parameters, unpack_calibration_parameters
+from .scenes import make_scenes
+
+__all__ = [
+    "BFGSSolver",
+    "line_search_wolfe_conditions",
+    "ReprojectionError",
+    "num_parameters",
+    "unpack_calibration_parameters",
+    "make_scenes",
+]

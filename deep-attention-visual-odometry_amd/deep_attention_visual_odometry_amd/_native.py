@@ -1,0 +1,123 @@
+"""ctypes binding of the C ABI in include/dava_ba.h (libdava_ba.so, gfx950).
+
+The library is built in-tree by ``make`` (see __graft_entry__.build()).  There
+is deliberately NO fallback: if the library or a ROCm device is missing, every
+product entry point raises.  torch is imported first so the library binds to
+the HIP runtime torch already loaded (both carry SONAME libamdhip64.so.7),
+which lets it run on torch's streams and torch-allocated memory.
+"""
+import ctypes
+import os
+import threading
+
+import torch  # noqa: F401  (must be loaded before the library, see above)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "_lib", "libdava_ba.so")
+
+DAVA_OK = 0
+DAVA_HESSIAN_DENSE = 0
+DAVA_HESSIAN_COMPACT = 1
+STOP_ITERATIONS, STOP_ERROR, STOP_STEP = 0, 1, 2
+STATUS_WORDS = 4
+
+_c_i64 = ctypes.c_int64
+_c_i32 = ctypes.c_int32
+_vp = ctypes.c_void_p
+
+
+class DavaScene(ctypes.Structure):
+    _fields_ = [
+        ("batch", _c_i32),
+        ("num_views", _c_i32),
+        ("num_points", _c_i32),
+        ("distortion", _c_i32),
+        ("num_parameters", _c_i32),
+        ("observations", _vp),
+        ("visibility", _vp),
+    ]
+
+
+class DavaSolverConfig(ctypes.Structure):
+    _fields_ = [
+        ("sufficient_decrease", ctypes.c_float),
+        ("curvature", ctypes.c_float),
+        ("error_threshold", ctypes.c_float),
+        ("minimum_step", ctypes.c_float),
+        ("iterations", _c_i32),
+        ("max_line_search_trials", _c_i32),
+        ("strong_wolfe", _c_i32),
+        ("hessian_mode", _c_i32),
+    ]
+
+
+# name -> (restype, argtypes); every symbol declared in include/dava_ba.h
+SIGNATURES = {
+    "dava_ba_solve_workspace_bytes": (ctypes.c_size_t, [ctypes.POINTER(DavaScene), ctypes.POINTER(DavaSolverConfig)]),
+    "dava_ba_solve": (ctypes.c_int, [ctypes.POINTER(DavaScene), ctypes.POINTER(DavaSolverConfig), _vp, _vp, _vp, _vp,
+                                     _vp, ctypes.c_size_t, _vp]),
+    "dava_ba_evaluate": (ctypes.c_int, [ctypes.POINTER(DavaScene), _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "dava_abi_version": (ctypes.c_int, []),
+    "dava_status_string": (ctypes.c_char_p, [ctypes.c_int]),
+    "dava_device_arch": (ctypes.c_char_p, []),
+}
+for _t in ("f32", "f64"):
+    _scalar = ctypes.c_float if _t == "f32" else ctypes.c_double
+    SIGNATURES.update({
+        f"dava_bfgs_update_inverse_hessian_{_t}": (ctypes.c_int, [_c_i64, _c_i64, _vp, _vp, _vp, _vp, _vp]),
+        f"dava_bfgs_initial_scale_{_t}": (ctypes.c_int, [_c_i64, _c_i64, _vp, _vp, _vp, _vp]),
+        f"dava_bfgs_scale_matrix_{_t}": (ctypes.c_int, [_c_i64, _c_i64, _vp, _vp, _vp, _vp]),
+        f"dava_bfgs_search_direction_{_t}": (ctypes.c_int, [_c_i64, _c_i64, _vp, _vp, _vp, _vp]),
+        f"dava_wolfe_init_{_t}": (ctypes.c_int, [_c_i64, _c_i64, _vp, _vp, _vp, _vp, _vp, _vp]),
+        f"dava_wolfe_propose_{_t}": (ctypes.c_int, [_c_i64, _vp, _vp, _vp]),
+        f"dava_wolfe_update_{_t}": (ctypes.c_int, [_c_i64, _c_i32, _scalar, _scalar, _c_i32, _vp, _vp, _vp]),
+    })
+
+_lock = threading.Lock()
+_lib = None
+
+
+class NativeLibraryError(RuntimeError):
+    pass
+
+
+def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
+    """Load and type the C ABI.  Raises NativeLibraryError if it is missing."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(path):
+            raise NativeLibraryError(
+                f"{path} not found: build it with `make -C deep-attention-visual-odometry_amd` "
+                "(or __graft_entry__.build()); there is no CPU fallback")
+        lib = ctypes.CDLL(path)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        if lib.dava_abi_version() != 1:
+            raise NativeLibraryError("libdava_ba.so ABI version mismatch")
+        _lib = lib
+        return lib
+
+
+def check(status: int, what: str) -> None:
+    if status != DAVA_OK:
+        msg = load_library().dava_status_string(status).decode()
+        raise RuntimeError(f"{what} failed: {msg} (status {status})")
+
+
+def require_device_tensor(t: torch.Tensor, what: str) -> None:
+    if not isinstance(t, torch.Tensor) or t.device.type != "cuda":
+        raise RuntimeError(
+            f"{what} must be a ROCm device tensor: this solver runs only on the GPU (no CPU fallback); "
+            f"got {getattr(t, 'device', type(t))}")
+
+
+def stream_of(device: torch.device):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def ptr(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())

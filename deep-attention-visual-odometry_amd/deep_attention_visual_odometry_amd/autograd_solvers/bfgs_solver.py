@@ -1,0 +1,168 @@
+"""Drop-in ``BFGSSolver`` (reference: ``autograd_solvers/bfgs_solver.py:26-303``).
+
+Same constructor keywords, defaults, ``forward(parameters, error_function)``
+contract, static methods and output conventions (functional, output
+``requires_grad`` iff the input's).  Two execution paths, both on the GPU:
+
+1. **Fused** -- ``error_function`` is a :class:`ReprojectionError` (the BA
+   objective of this project's hot path): the entire solve -- objective,
+   gradient, inverse-Hessian updates, strong-Wolfe line search, stopping
+   rules -- is ONE launch of ``dava_ba_solve`` (include/dava_ba.h).
+2. **Generic closure** -- any other ``error_function(parameters, mask)``:
+   the closure and ``torch.autograd.grad`` run in PyTorch on the device;
+   the inverse-Hessian scale/update, search direction and the line-search
+   state machine run in the library's HIP kernels.  The loop mirrors
+   ``bfgs_solver.py:118-212`` including the mask contract of ``:99-104``.
+
+Not supported (raises rather than silently falling back): CPU tensors and
+differentiating through the solve (``parameters.requires_grad``; the
+reference's ``create_graph`` mode).
+"""
+from typing import Callable, Optional
+
+import torch
+from torch.nn import Module
+
+from .. import _native, native_ops
+from ..camera_model import ReprojectionError
+from .line_search import line_search_wolfe_conditions
+
+
+class BFGSSolver(Module):
+    """Broyden-Fletcher-Goldfarb-Shanno with a dense inverse Hessian per problem and a
+    strong-Wolfe line search (Nocedal & Wright 2009, eq. 6.17, 6.20; alg. 3.5/3.6)."""
+
+    def __init__(
+        self,
+        sufficient_decrease: float = 1e-4,
+        curvature: float = 0.9,
+        error_threshold: float = 1e-4,
+        iterations: int = 1000,
+        minimum_step: float = 1e-8,
+        drop_path_p: float = 0.1,
+        return_second_last: bool = False,
+        training_iterations: int = None,
+        training_error_threshold: float = None,
+        hessian_mode: str = "dense",
+    ):
+        super().__init__()
+        self.sufficient_decrease = float(sufficient_decrease)
+        self.curvature = float(curvature)
+        self.error_threshold = float(error_threshold)
+        self.iterations = int(iterations)
+        self.minimum_step = float(minimum_step)
+        self.drop_path_p = float(drop_path_p)
+        self.return_second_last = bool(return_second_last)
+        self.training_iterations = int(training_iterations) if training_iterations is not None else self.iterations
+        self.training_error_threshold = (
+            float(training_error_threshold) if training_error_threshold is not None else self.error_threshold
+        )
+        if hessian_mode not in ("dense", "compact"):
+            raise ValueError("hessian_mode must be 'dense' or 'compact'")
+        self.hessian_mode = hessian_mode
+        self.last_status: Optional[torch.Tensor] = None
+
+    # ---- public static helpers (bfgs_solver.py:217-303) ----
+    @staticmethod
+    def scale_initial_inverse_hessian(step: torch.Tensor, delta_gradient: torch.Tensor) -> torch.Tensor:
+        return native_ops.initial_scale(step, delta_gradient)
+
+    @staticmethod
+    def update_inverse_hessian(inverse_hessian: torch.Tensor, step: torch.Tensor,
+                               delta_gradient: torch.Tensor) -> torch.Tensor:
+        return native_ops.update_inverse_hessian(inverse_hessian, step, delta_gradient)
+
+    # ---- forward ----
+    def forward(self, parameters: torch.Tensor,
+                error_function: Callable[[torch.Tensor, torch.Tensor], torch.Tensor]) -> torch.Tensor:
+        _native.require_device_tensor(parameters, "parameters")
+        if parameters.requires_grad:
+            raise NotImplementedError(
+                "differentiating through the solve (parameters.requires_grad, the reference's create_graph mode) "
+                "is not implemented on the GPU path yet; detach the initial guess")
+        if self.training:
+            error_threshold, num_iterations = self.training_error_threshold, self.training_iterations
+        else:
+            error_threshold, num_iterations = self.error_threshold, self.iterations
+        stochastic = self.training and (self.drop_path_p > 0.0 or self.return_second_last)
+        if isinstance(error_function, ReprojectionError) and not stochastic:
+            return self._fused(parameters, error_function, error_threshold, num_iterations)
+        return self._generic(parameters, error_function, error_threshold, num_iterations)
+
+    def _fused(self, parameters, fn: ReprojectionError, error_threshold, num_iterations):
+        lead = parameters.shape[:-1]
+        if fn.batch_shape != lead:
+            raise ValueError(f"ReprojectionError batch shape {tuple(fn.batch_shape)} != parameters {tuple(lead)}")
+        x0 = parameters.reshape(-1, parameters.size(-1))
+        if x0.dtype != torch.float32:
+            raise TypeError("the fused BA solver computes in float32")
+        mode = _native.DAVA_HESSIAN_DENSE if self.hessian_mode == "dense" else _native.DAVA_HESSIAN_COMPACT
+        x, _, status = native_ops.ba_solve(
+            x0, fn.observations.reshape(-1, fn.num_views, fn.num_points, 2),
+            fn.visibility.reshape(-1, fn.num_views, fn.num_points), fn.num_views, fn.num_points, fn.distortion,
+            sufficient_decrease=self.sufficient_decrease, curvature=self.curvature,
+            error_threshold=error_threshold, iterations=num_iterations, minimum_step=self.minimum_step,
+            hessian_mode=mode, want_status=True)
+        self.last_status = status
+        return x.reshape(parameters.shape)
+
+    def _generic(self, parameters, error_function, error_threshold, num_iterations):
+        batch_dimensions = parameters.shape[:-1]
+        parameter_dim = parameters.size(-1)
+        device = parameters.device
+        updating = torch.ones(batch_dimensions, dtype=torch.bool, device=device)
+
+        def wrapped(inner_parameters: torch.Tensor, inner_mask: torch.Tensor) -> torch.Tensor:
+            mask = torch.zeros_like(updating)
+            mask[updating] = inner_mask
+            return error_function(inner_parameters, mask)
+
+        parameters = parameters.detach()
+        step = torch.zeros_like(parameters)
+        error = torch.empty(batch_dimensions, dtype=parameters.dtype, device=device)
+        gradient = torch.empty_like(parameters)
+        inverse_hessian = torch.zeros(batch_dimensions + (parameter_dim, parameter_dim), dtype=parameters.dtype,
+                                      device=device)
+        inverse_hessian[..., range(parameter_dim), range(parameter_dim)] = 1.0
+        for step_idx in range(num_iterations):
+            prev_gradient = gradient
+            if self.training and self.drop_path_p > 0.0:
+                updating = updating & torch.greater(torch.rand_like(updating, dtype=torch.float32), self.drop_path_p)
+            upd_params = parameters[updating].requires_grad_(True)
+            with torch.enable_grad():
+                upd_error = error_function(upd_params, updating)
+                (upd_grad,) = torch.autograd.grad(upd_error.sum(), upd_params)
+            error = error.masked_scatter(updating, upd_error.detach())
+            gradient = gradient.masked_scatter(updating.unsqueeze(-1).expand_as(gradient), upd_grad)
+            updating = updating & torch.greater(error, error_threshold)
+            if not bool(torch.any(updating)):
+                break
+            upd_params = parameters[updating]
+            upd_error = error[updating]
+            upd_grad = gradient[updating]
+            if step_idx == 0:
+                direction = -1.0 * upd_grad
+            else:
+                delta = upd_grad - prev_gradient[updating]
+                upd_h = inverse_hessian[updating]
+                upd_step = step[updating]
+                if step_idx == 1:
+                    upd_h = native_ops.scale_matrix(native_ops.initial_scale(upd_step, delta), upd_h)
+                upd_h = native_ops.update_inverse_hessian(upd_h, upd_step, delta)
+                direction = native_ops.search_direction(upd_h, upd_grad)
+                inverse_hessian = inverse_hessian.masked_scatter(
+                    updating.unsqueeze(-1).unsqueeze(-1).expand_as(inverse_hessian), upd_h)
+            step_size = line_search_wolfe_conditions(
+                upd_params, direction, upd_error, upd_grad, wrapped,
+                sufficient_decrease=self.sufficient_decrease, curvature=self.curvature, strong=True)
+            upd_step = step_size.unsqueeze(-1) * direction
+            new_params = upd_params + upd_step
+            step = step.masked_scatter(updating.unsqueeze(-1).expand_as(step), upd_step)
+            if not self.training or not self.return_second_last:
+                parameters = parameters.masked_scatter(updating.unsqueeze(-1).expand_as(parameters), new_params)
+            updating = updating & torch.greater(torch.linalg.vector_norm(step, dim=-1), self.minimum_step)
+            if not bool(torch.any(updating)):
+                break
+            if self.training and self.return_second_last:
+                parameters = parameters.masked_scatter(updating.unsqueeze(-1).expand_as(parameters), new_params)
+        return parameters.detach()

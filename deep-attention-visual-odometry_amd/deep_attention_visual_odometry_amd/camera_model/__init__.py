@@ -1,0 +1,110 @@
+"""Calibration parameter layout and the native reprojection objective.
+
+``unpack_calibration_parameters`` mirrors
+``camera_model/calibration_pinhole_camera_model.py:33-75`` (same names,
+same shapes, same ValueError on a wrong P).  ``ReprojectionError`` is the
+error-function object the drop-in ``BFGSSolver`` recognises and runs fully
+fused on the GPU; it is also an ordinary ``error_function(parameters,
+batch_mask)`` closure (``networks/calibration_network.py:58-67`` contract)
+whose value and first derivative come from the HIP objective kernel, so it
+works with any caller that only needs first-order autograd.
+"""
+from typing import NamedTuple
+
+import torch
+
+from .. import native_ops
+
+
+def num_parameters(num_views: int, num_points: int, distortion: bool = False) -> int:
+    return 3 + 3 * num_points + 6 * (num_views - 1) + (5 if distortion else 0)
+
+
+class CalibrationParameters(NamedTuple):
+    intrinsics: torch.Tensor
+    world_points: torch.Tensor
+    camera_translations: torch.Tensor
+    camera_rotations: torch.Tensor
+
+
+def unpack_calibration_parameters(parameters: torch.Tensor, num_views: int, num_points: int) -> CalibrationParameters:
+    """Views of a (B..., 3 + 3N + 6(M-1)) parameter tensor (pinhole layout)."""
+    expected = 3 + 3 * num_points + 6 * (num_views - 1)
+    if parameters.size(-1) != expected:
+        raise ValueError(
+            f"The final dimension of the input tensor must be 3 + 3 * num_points + 6 * (num_views - 1) = "
+            f"{expected}, got {parameters.size(-1)}")
+    lead = parameters.shape[:-1]
+    p_end = 3 + 3 * num_points
+    t_end = p_end + 3 * (num_views - 1)
+    return CalibrationParameters(
+        intrinsics=parameters[..., 0:3].reshape(lead + (1, 1, 3)),
+        world_points=parameters[..., 3:p_end].reshape(lead + (1, num_points, 3)),
+        camera_translations=parameters[..., p_end:t_end].reshape(lead + (num_views - 1, 1, 3)),
+        camera_rotations=parameters[..., t_end:].reshape(lead + (num_views - 1, 1, 3)),
+    )
+
+
+class _NativeObjective(torch.autograd.Function):
+    """E(x) per row with dE/dx from the HIP reverse-mode kernel (first order only)."""
+
+    @staticmethod
+    def forward(ctx, x, observations, visibility, num_views, num_points, distortion):
+        err, grad, _ = native_ops.ba_evaluate(x, observations, visibility, num_views, num_points, distortion,
+                                              want_grad=ctx.needs_input_grad[0])
+        ctx.save_for_backward(grad if grad is not None else err)
+        return err
+
+    @staticmethod
+    @torch.autograd.function.once_differentiable
+    def backward(ctx, grad_out):
+        (grad,) = ctx.saved_tensors
+        return grad_out.unsqueeze(-1) * grad, None, None, None, None, None
+
+
+class ReprojectionError:
+    """Squared multi-view reprojection error of SURVEY.md 8(a).
+
+    E(x) = sum_{m,n} vis[m,n] || pi_m(X_n) - obs[m,n] ||^2
+
+    observations: (B..., M, N, 2) float32, visibility: (B..., M, N) bool/0-1,
+    on the same ROCm device as the parameters.  With ``distortion=True`` the
+    five Brown-Conrady coefficients (k1 k2 k3 p1 p2) are appended to the
+    parameter vector (``camera_model/distorted_camera_model.py:59-86``).
+    """
+
+    def __init__(self, observations: torch.Tensor, visibility: torch.Tensor, num_views: int, num_points: int,
+                 distortion: bool = False):
+        if observations.shape[-3:] != (num_views, num_points, 2):
+            raise ValueError(f"observations must end in ({num_views}, {num_points}, 2), got {tuple(observations.shape)}")
+        if visibility.shape != observations.shape[:-1]:
+            raise ValueError("visibility must have shape observations.shape[:-1]")
+        if num_views < 2:
+            raise ValueError("num_views must be >= 2")
+        self.observations = observations.to(torch.float32)
+        self.visibility = visibility.to(torch.uint8)
+        self.num_views = int(num_views)
+        self.num_points = int(num_points)
+        self.distortion = bool(distortion)
+
+    @property
+    def num_parameters(self) -> int:
+        return num_parameters(self.num_views, self.num_points, self.distortion)
+
+    @property
+    def batch_shape(self) -> torch.Size:
+        return self.observations.shape[:-3]
+
+    def __call__(self, parameters: torch.Tensor, batch_mask: torch.Tensor) -> torch.Tensor:
+        if parameters.size(-1) != self.num_parameters:
+            raise ValueError(f"expected {self.num_parameters} parameters, got {parameters.size(-1)}")
+        obs = self.observations[batch_mask]
+        vis = self.visibility[batch_mask]
+        lead = parameters.shape[:-1]
+        x = parameters.reshape(-1, parameters.size(-1))
+        obs = obs.reshape(-1, self.num_views, self.num_points, 2)
+        vis = vis.reshape(-1, self.num_views, self.num_points)
+        if x.dtype != torch.float32:
+            raise TypeError("ReprojectionError evaluates in float32")
+        err = _NativeObjective.apply(x, obs, vis, self.num_views, self.num_points, self.distortion)
+        return err.reshape(lead)

@@ -6,25 +6,35 @@ reference snapshot) with a deterministic one: problem ``i`` of a batch is a
 pure function of ``(seed, i)``, so any contiguous shard of a batch can be
 generated on its own rank with no scatter.
 
-Distributions (per problem):
+Distributions (per problem), in camera 0's frame:
 
 * f = 1/tan(a/2), a ~ U(pi/6, 2pi/3)                 (dataset ``:148-150``)
 * cx, cy ~ clamp(0.2 N(0,1), -0.5, 0.5)               (``:149``)
-* X_xy ~ N(0, 3^2), X_z ~ |20 + 5 N(0,1)|             (``:90-94``)
-* t_m ~ N(0, 3^2), w_m ~ N(0, 0.3^2)                  (``:110``)
+* X_xy ~ N(0, 3^2), X_z = 20 + 5 clip(N(0,1), -3, 3)  (``:90-94``, clipped so no
+  point sits on a camera plane)
+* views m >= 1 look at the cloud, like the dataset's look-at construction
+  (``:100-133``): centre C_m ~ N(0, 3^2), target (0, 0, 20) + N(0, 1), roll
+  ~ N(0, 0.1^2); stored as axis-angle w_m and t_m = -R(w_m) C_m
 * k1 ~ N(0, 1e-2^2), k2 ~ N(0, 1e-3^2), k3 ~ N(0, 1e-4^2), p1, p2 ~ N(0, 1e-3^2)
 * observations: noise-free projection of the truth (fp64, then fp32)
-* visibility: |u| < 1 and |v| < 1 (``:194-197``) or all-true (roofline runs)
+* visibility: |u| < 1 and |v| < 1 (``:194-197``) or all-true
 * initial guess x0 = truth + N(0, 0.01^2) on the pinhole block; the five
   distortion coefficients get 10 % of their own spread
   (N(0, [1e-3, 1e-4, 1e-5, 1e-4, 1e-4]^2)) -- a 0.01 kick on k3 (spread 1e-4)
   is 100 sigma and sends k3 r^6 to ~1e2 at the image edge.
+
+Why look-at views: with independent random rotations (no look-at) many
+cameras face away from the cloud, points land near a camera plane, and
+invisible pairs overflow (inf * vis 0 = NaN poisons E in the reference's
+objective too); two-view problems also become so ill-conditioned that the
+reference's own fp32 trajectory changes by 1e-4 under a 1-ulp input nudge.
 
 Parameter layout: see ``camera_model.layout``.
 """
 from typing import NamedTuple
 
 import numpy as np
+from scipy.spatial.transform import Rotation
 
 
 class SceneBatch(NamedTuple):
@@ -49,6 +59,16 @@ def _rotate(v: np.ndarray, w: np.ndarray) -> np.ndarray:
     k = w / theta
     c, s = np.cos(theta), np.sin(theta)
     return v * c + np.cross(k, v) * s + np.outer(v @ k, k) * (1.0 - c)
+
+
+def _look_at(forward: np.ndarray, roll: float) -> Rotation:
+    """Rotation R with R forward/|forward| = +z, followed by a roll about +z."""
+    f = forward / np.linalg.norm(forward)
+    axis = np.cross(f, np.array([0.0, 0.0, 1.0]))
+    sin_a = np.linalg.norm(axis)
+    angle = np.arctan2(sin_a, f[2])
+    align = Rotation.from_rotvec(axis / sin_a * angle) if sin_a > 1e-12 else Rotation.identity()
+    return Rotation.from_rotvec([0.0, 0.0, roll]) * align
 
 
 def project_truth(x: np.ndarray, num_views: int, num_points: int, distortion: bool) -> np.ndarray:
@@ -99,9 +119,15 @@ def make_scenes(
         f = 1.0 / np.tan(a / 2.0)
         c = np.clip(0.2 * rng.standard_normal(2), -0.5, 0.5)
         xy = 3.0 * rng.standard_normal((num_points, 2))
-        z = np.abs(20.0 + 5.0 * rng.standard_normal((num_points, 1)))
-        t = 3.0 * rng.standard_normal((num_views - 1, 3))
-        w = 0.3 * rng.standard_normal((num_views - 1, 3))
+        z = 20.0 + 5.0 * np.clip(rng.standard_normal((num_points, 1)), -3.0, 3.0)
+        t = np.empty((num_views - 1, 3))
+        w = np.empty((num_views - 1, 3))
+        for m in range(num_views - 1):
+            centre = 3.0 * rng.standard_normal(3)
+            target = np.array([0.0, 0.0, 20.0]) + rng.standard_normal(3)
+            rot = _look_at(target - centre, 0.1 * rng.standard_normal())
+            w[m] = rot.as_rotvec()
+            t[m] = -rot.apply(centre)
         row = [np.array([f, c[0], c[1]]), np.concatenate([xy, z], axis=1).ravel(), t.ravel(), w.ravel()]
         if distortion:
             row.append(rng.standard_normal(5) * np.array([1e-2, 1e-3, 1e-4, 1e-3, 1e-3]))

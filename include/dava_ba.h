@@ -1,0 +1,176 @@
+/*
+ * dava_ba.h -- C ABI of the MI355X (gfx950) batched BFGS bundle-adjustment solver.
+ *
+ * This is the drop-in boundary for the one hot path of
+ * jskinn/deep-attention-visual-odometry that this project replaces: the
+ * `autograd_solvers/` BFGS loop + strong-Wolfe line search evaluated on a
+ * multi-view pinhole (+ Brown-Conrady) reprojection objective.  The reference
+ * is pure PyTorch (no FFI exists there); each entry point below names the
+ * reference interface it replaces.  The Python mirror of the reference API
+ * (deep_attention_visual_odometry_amd.autograd_solvers) binds these symbols
+ * through ctypes; INTEGRATION.md shows the binding a maintainer would add.
+ *
+ * Conventions
+ *  - Every pointer is a DEVICE pointer (HBM) unless stated otherwise.
+ *    Struct arguments themselves are host memory.
+ *  - `stream` is a hipStream_t (NULL = default stream); all work is
+ *    enqueued asynchronously on it, nothing synchronises the host, and no
+ *    entry point allocates memory (caller supplies the workspace), so every
+ *    call is graph-capturable.
+ *  - Functional ownership, like the reference (`bfgs_solver.py:197`):
+ *    inputs are never written; outputs may not alias inputs unless stated.
+ *  - Return value: DAVA_OK or a DAVA_ERR_* code; nothing throws across the ABI.
+ *    dava_status_string() turns a code into text.
+ *  - fp32 throughout the fused solver (the reference's dtype for the BA path);
+ *    the generic BFGS building blocks come in _f32 and _f64 flavours because
+ *    the reference's own unit tests drive them in float64.
+ */
+#ifndef DAVA_BA_H
+#define DAVA_BA_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DAVA_ABI_VERSION 1
+
+enum DavaStatus {
+  DAVA_OK = 0,
+  DAVA_ERR_INVALID_ARGUMENT = 1, /* bad sizes / null pointers / P mismatch  */
+  DAVA_ERR_WORKSPACE = 2,        /* workspace missing or too small          */
+  DAVA_ERR_LAUNCH = 3,           /* HIP launch failure                      */
+  DAVA_ERR_UNSUPPORTED = 4       /* shape outside what this build supports  */
+};
+
+/* Representation of the inverse Hessian inside the fused solver. */
+enum DavaHessianMode {
+  DAVA_HESSIAN_DENSE = 0,  /* dense P x P fp32 per problem in HBM (the reference's data structure) */
+  DAVA_HESSIAN_COMPACT = 1 /* exact rank-2 update history (s_j, H_{j-1} y_j): same math, O(kP) bytes */
+};
+
+/* Why a problem stopped (bfgs_solver.py:143-145, :203-207). */
+enum DavaStopReason {
+  DAVA_STOP_ITERATIONS = 0, /* ran `iterations` steps                 */
+  DAVA_STOP_ERROR = 1,      /* error <= error_threshold (or NaN)      */
+  DAVA_STOP_STEP = 2        /* ||step|| <= minimum_step (or NaN)      */
+};
+
+/* A batch of independent calibration problems.
+ * Parameter layout per problem (calibration_pinhole_camera_model.py:33-75):
+ *   [f, cx, cy | X_0..X_{N-1} (xyz) | t_1..t_{M-1} | w_1..w_{M-1} | k1 k2 k3 p1 p2 (if distortion)]
+ * num_parameters must equal 3 + 3N + 6(M-1) + 5*distortion.                     */
+typedef struct DavaScene {
+  int32_t batch;               /* B >= 0                               */
+  int32_t num_views;           /* M >= 2                               */
+  int32_t num_points;          /* N >= 1                               */
+  int32_t distortion;          /* 0 = pinhole, 1 = + Brown-Conrady     */
+  int32_t num_parameters;      /* P                                    */
+  const float* observations;   /* (B, M, N, 2) fp32                    */
+  const uint8_t* visibility;   /* (B, M, N) 0/1                        */
+} DavaScene;
+
+/* Mirrors the eval-mode BFGSSolver constructor (bfgs_solver.py:49-78). */
+typedef struct DavaSolverConfig {
+  float sufficient_decrease;      /* c1, default 1e-4                          */
+  float curvature;                /* c2, default 0.9                           */
+  float error_threshold;          /* default 1e-4                              */
+  float minimum_step;             /* default 1e-8                              */
+  int32_t iterations;             /* default 1000                              */
+  int32_t max_line_search_trials; /* 1000 in wolfe_conditions.py:116           */
+  int32_t strong_wolfe;           /* 1 (bfgs_solver.py:189)                    */
+  int32_t hessian_mode;           /* DavaHessianMode                           */
+} DavaSolverConfig;
+
+/* Per-problem status written by dava_ba_solve: int32 (B, 4) =
+ * {steps taken, DavaStopReason, objective evaluations, line-search trials}. */
+#define DAVA_STATUS_WORDS 4
+
+/* Bytes of device workspace dava_ba_solve needs for this scene/config. */
+size_t dava_ba_solve_workspace_bytes(const DavaScene* scene, const DavaSolverConfig* config);
+
+/* The whole eval-mode solve, one launch.
+ * Replaces BFGSSolver.forward(parameters, error_function)
+ * (autograd_solvers/bfgs_solver.py:80-215) with error_function = the squared
+ * reprojection objective over `scene`, including line_search_wolfe_conditions
+ * (autograd_solvers/line_search/wolfe_conditions.py:23-239, strong=True).
+ *   x0        (B, P) fp32 initial guess
+ *   x_out     (B, P) fp32 result (may alias x0)
+ *   error_out (B)    fp32 objective at x_out, or NULL
+ *   status_out(B, 4) int32, or NULL                                         */
+int dava_ba_solve(const DavaScene* scene, const DavaSolverConfig* config, const float* x0, float* x_out,
+                  float* error_out, int32_t* status_out, void* workspace, size_t workspace_bytes,
+                  void* stream);
+
+/* One objective evaluation per problem at x + alpha[b] * direction.
+ * Replaces one call of the reference-composed error function plus
+ * torch.autograd.grad (bfgs_solver.py:131-135 / wolfe_conditions.py:134-143):
+ *   direction (B, P) or NULL (then alpha is ignored and the point is x)
+ *   alpha     (B)    or NULL (= 0)
+ *   error_out (B)    E
+ *   grad_out  (B, P) dE/dx at the point, or NULL
+ *   slope_out (B)    d . dE/dx at the point (forward mode), or NULL (needs direction) */
+int dava_ba_evaluate(const DavaScene* scene, const float* x, const float* direction, const float* alpha,
+                     float* error_out, float* grad_out, float* slope_out, void* stream);
+
+/* ---- generic BFGS building blocks (drive an arbitrary error closure) ----
+ * batch = number of problems (all leading dims flattened), n = P.          */
+
+/* BFGSSolver.update_inverse_hessian (bfgs_solver.py:235-303): h, h_out (batch,n,n); s, y (batch,n). */
+int dava_bfgs_update_inverse_hessian_f32(int64_t batch, int64_t n, const float* h, const float* s,
+                                         const float* y, float* h_out, void* stream);
+int dava_bfgs_update_inverse_hessian_f64(int64_t batch, int64_t n, const double* h, const double* s,
+                                         const double* y, double* h_out, void* stream);
+
+/* BFGSSolver.scale_initial_inverse_hessian (bfgs_solver.py:217-233): scale_out (batch). */
+int dava_bfgs_initial_scale_f32(int64_t batch, int64_t n, const float* s, const float* y, float* scale_out,
+                                void* stream);
+int dava_bfgs_initial_scale_f64(int64_t batch, int64_t n, const double* s, const double* y,
+                                double* scale_out, void* stream);
+
+/* h_out = scale[b] * h (batch,n,n): the k==1 rescale (bfgs_solver.py:159-167). May alias. */
+int dava_bfgs_scale_matrix_f32(int64_t batch, int64_t n, const float* scale, const float* h, float* h_out,
+                               void* stream);
+int dava_bfgs_scale_matrix_f64(int64_t batch, int64_t n, const double* scale, const double* h,
+                               double* h_out, void* stream);
+
+/* d_out = -H g (bfgs_solver.py:173-176). */
+int dava_bfgs_search_direction_f32(int64_t batch, int64_t n, const float* h, const float* g, float* d_out,
+                                   void* stream);
+int dava_bfgs_search_direction_f64(int64_t batch, int64_t n, const double* h, const double* g,
+                                   double* d_out, void* stream);
+
+/* Strong/weak Wolfe line-search state machine (wolfe_conditions.py:23-239),
+ * batched, for an error function evaluated by the caller between calls.
+ * state (batch, 9): {a_lo, a_hi, a, f_lo, f_hi, f_a, dphi_a, f0, dphi0}
+ * flags (batch, 2) uint8: {widening, zooming}
+ *   init:    dphi0 = direction . g0, a = 1, brackets 0, errors f0; widening.
+ *   propose: (trial > 0) widening: a_hi = a, f_hi = f_a, a *= 2;
+ *            zooming: a = (a_lo + a_hi) / 2.
+ *   update:  after the caller wrote f(a) into column 5 and phi'(a) into
+ *            column 6 for the active rows, apply N&W 3.5/3.6.
+ * The search result is column 1 (a_hi).                                    */
+int dava_wolfe_init_f32(int64_t batch, int64_t n, const float* direction, const float* f0, const float* g0,
+                        float* state, uint8_t* flags, void* stream);
+int dava_wolfe_init_f64(int64_t batch, int64_t n, const double* direction, const double* f0,
+                        const double* g0, double* state, uint8_t* flags, void* stream);
+int dava_wolfe_propose_f32(int64_t batch, float* state, const uint8_t* flags, void* stream);
+int dava_wolfe_propose_f64(int64_t batch, double* state, const uint8_t* flags, void* stream);
+int dava_wolfe_update_f32(int64_t batch, int32_t trial, float c1, float c2, int32_t strong, float* state,
+                          uint8_t* flags, void* stream);
+int dava_wolfe_update_f64(int64_t batch, int32_t trial, double c1, double c2, int32_t strong, double* state,
+                          uint8_t* flags, void* stream);
+
+/* ---- misc ---- */
+const char* dava_status_string(int status);
+int dava_abi_version(void);
+/* Compiled-in device architecture, e.g. "gfx950". */
+const char* dava_device_arch(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* DAVA_BA_H */

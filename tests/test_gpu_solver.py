@@ -1,0 +1,145 @@
+"""Fused HIP solve (dava_ba_solve via the drop-in BFGSSolver) vs the CPU oracle.
+
+Parity bar (north_star / SURVEY.md 8(d)): per-problem normwise
+||x_gpu - x_ref|| / ||x_ref|| <= 1e-5 after a fixed K <= 100 iterations, fp32.
+The reference's own sensitivity to a 2-ulp input perturbation is ~1.4e-6 at
+K = 100, so 1e-5 leaves room for the different reduction
+order of the kernel.  Intrinsics (f, cx, cy) are also compared on their own,
+against max(1e-5, 10 x the oracle's own change under a 1-ulp nudge of x0):
+for a few ill-conditioned problems the reference itself moves f by more than
+1e-5 under such a nudge, and no fp32 implementation can be closer than that.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN
+from oracle import objective, solver
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-5
+
+
+def _scene(b, m, n, distortion, seed):
+    from deep_attention_visual_odometry_amd import make_scenes
+
+    s = make_scenes(b, m, n, distortion=distortion, seed=seed)
+    return torch.tensor(s.initial), torch.tensor(s.observations), torch.tensor(s.visibility)
+
+
+def _gpu_solve(device, x0, obs, vis, m, n, distortion, **kw):
+    from deep_attention_visual_odometry_amd import BFGSSolver, ReprojectionError
+
+    fn = ReprojectionError(obs.to(device), vis.to(device), m, n, distortion)
+    s = BFGSSolver(**kw).eval()
+    out = s(x0.to(device), fn).cpu()
+    return out, s.last_status.cpu()
+
+
+def _rel(a, b):
+    return ((a.double() - b.double()).norm(dim=-1) / b.double().norm(dim=-1))
+
+
+def _intrinsics_envelope(x0, fn, ref, **kw):
+    """Per-problem 10x the oracle's own intrinsics change under a 1-ulp nudge of x0 (floor 1e-5)."""
+    nudged = solver.bfgs_solve(torch.nextafter(x0, torch.full_like(x0, float("inf"))), fn, **kw)
+    return torch.clamp(10.0 * _rel(nudged[:, :3], ref[:, :3]), min=TOL)
+
+
+@pytest.mark.parametrize("m,n,distortion,k,b", [
+    (2, 64, False, 5, 8), (2, 64, False, 20, 8), (2, 64, False, 100, 4),
+    (2, 128, False, 20, 4), (2, 128, False, 100, 2),
+    (4, 256, False, 20, 2), (4, 256, True, 20, 2),
+])
+def test_fixed_iterations_match_oracle(device, m, n, distortion, k, b):
+    x0, obs, vis = _scene(b, m, n, distortion, 100 + k + n)
+    out, status = _gpu_solve(device, x0, obs, vis, m, n, distortion, iterations=k, error_threshold=-1.0,
+                             minimum_step=-1.0)
+    rec = solver.SolveRecord(None, None)
+    fn = objective.ReprojectionClosure(obs, vis, m, n, distortion)
+    kw = dict(iterations=k, error_threshold=-1.0, minimum_step=-1.0)
+    ref = solver.bfgs_solve(x0, fn, record=rec, **kw)
+    rel = _rel(out, ref)
+    assert rel.max() <= TOL, rel
+    assert (_rel(out[:, :3], ref[:, :3]) <= _intrinsics_envelope(x0, fn, ref, **kw)).all()
+    assert torch.equal(status[:, 0], rec.iterations)
+    assert (status[:, 1] == 0).all()
+
+
+@pytest.mark.parametrize("case,ks", [("c1", (5, 20, 100)), ("c2", (5, 20, 100)), ("c3", (5, 20))])
+def test_reference_golden_trajectories(device, case, ks):
+    """Against BFGSSolver().eval() outputs of the REAL reference (tests/golden/bfgs_traj.npz)."""
+    g = np.load(os.path.join(GOLDEN, "bfgs_traj.npz"))
+    m, n = {"c1": (2, 64), "c2": (2, 128), "c3": (4, 256)}[case]
+    x0 = torch.tensor(g[case + "_x0"])
+    obs, vis = torch.tensor(g[case + "_obs"]), torch.tensor(g[case + "_vis"])
+    for k in ks:
+        out, _ = _gpu_solve(device, x0, obs, vis, m, n, False, iterations=k, error_threshold=-1.0,
+                            minimum_step=-1.0)
+        ref = torch.tensor(g[f"{case}_k{k}"])
+        assert _rel(out, ref).max() <= TOL, (case, k, _rel(out, ref))
+
+
+def test_default_stopping_rules(device):
+    """Reference defaults (error 1e-4, 1000 iterations, min step 1e-8): the objective reached
+    matches the oracle's, and every problem stops by a rule, not the cap."""
+    x0, obs, vis = _scene(4, 2, 64, False, 321)
+    out, status = _gpu_solve(device, x0, obs, vis, 2, 64, False)
+    fn = objective.ReprojectionClosure(obs, vis, 2, 64)
+    rec = solver.SolveRecord(None, None)
+    ref = solver.bfgs_solve(x0, fn, record=rec)
+    e_gpu = objective.reprojection_error(out.double(), obs.double(), vis, 2, 64)
+    e_ref = objective.reprojection_error(ref.double(), obs.double(), vis, 2, 64)
+    assert (e_gpu <= 1e-4 + 1e-6).all() or (status[:, 1] != 0).all()
+    assert (status[:, 1] != 0).all()
+    assert torch.allclose(e_gpu, e_ref, rtol=0.5, atol=1e-4)
+
+
+def test_error_threshold_stops_immediately(device):
+    x0, obs, vis = _scene(3, 2, 64, False, 5)
+    out, status = _gpu_solve(device, x0, obs, vis, 2, 64, False, error_threshold=1e30)
+    assert torch.equal(out, x0)
+    assert (status[:, 0] == 0).all() and (status[:, 1] == 1).all() and (status[:, 2] == 1).all()
+
+
+def test_zero_iterations_returns_input(device):
+    x0, obs, vis = _scene(2, 2, 64, False, 6)
+    out, status = _gpu_solve(device, x0, obs, vis, 2, 64, False, iterations=0)
+    assert torch.equal(out, x0)
+    assert (status[:, 0] == 0).all()
+
+
+def test_batch_dimensions_and_problem_independence(device):
+    """(2, 3, P) batches give the same per-problem results as solving each alone."""
+    from deep_attention_visual_odometry_amd import BFGSSolver, ReprojectionError
+
+    x0, obs, vis = _scene(6, 2, 64, False, 7)
+    fn = ReprojectionError(obs.reshape(2, 3, 2, 64, 2).to(device), vis.reshape(2, 3, 2, 64).to(device), 2, 64)
+    s = BFGSSolver(iterations=15, error_threshold=-1.0, minimum_step=-1.0).eval()
+    out = s(x0.reshape(2, 3, -1).to(device), fn).cpu()
+    assert out.shape == (2, 3, x0.shape[-1])
+    single, _ = _gpu_solve(device, x0[4:5], obs[4:5], vis[4:5], 2, 64, False, iterations=15, error_threshold=-1.0,
+                           minimum_step=-1.0)
+    assert torch.equal(out.reshape(6, -1)[4], single[0])
+
+
+def test_error_decreases_and_converges_large_batch(device):
+    """Size-independent properties at a larger batch: objective never increases vs the
+    start, and most problems get close to the truth."""
+    from deep_attention_visual_odometry_amd import make_scenes, native_ops
+
+    s = make_scenes(256, 4, 256, distortion=True, seed=2024)
+    x0 = torch.tensor(s.initial).to(device)
+    obs = torch.tensor(s.observations).to(device)
+    vis = torch.tensor(s.visibility).to(device)
+    out, err, status = native_ops.ba_solve(x0, obs, vis, 4, 256, True, iterations=100, error_threshold=-1.0,
+                                           minimum_step=-1.0, want_error=True, want_status=True)
+    e0, _, _ = native_ops.ba_evaluate(x0, obs, vis, 4, 256, True, want_grad=False)
+    assert (err <= e0).all()
+    assert torch.isfinite(out).all()
+    assert (err < 1e-3 * e0).float().mean() > 0.9
+    assert (status[:, 0] == 100).all()
+    assert (status[:, 2] > 100).all()

@@ -1,0 +1,106 @@
+"""The C-ABI library loads and exports exactly what include/dava_ba.h declares (CPU only).
+
+No compute is launched here: only argument validation paths that return
+before touching a device."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from conftest import REPO
+
+
+def _declared_symbols():
+    text = open(os.path.join(REPO, "include", "dava_ba.h")).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(dava_[a-z0-9_]+)\s*\(", text)))
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from deep_attention_visual_odometry_amd import _native
+
+    return _native.load_library()
+
+
+def test_header_declares_the_expected_entry_points():
+    syms = _declared_symbols()
+    for name in ("dava_ba_solve", "dava_ba_solve_workspace_bytes", "dava_ba_evaluate",
+                 "dava_bfgs_update_inverse_hessian_f32", "dava_bfgs_update_inverse_hessian_f64",
+                 "dava_wolfe_update_f32", "dava_abi_version"):
+        assert name in syms
+
+
+def test_library_exports_every_declared_symbol(lib):
+    missing = [s for s in _declared_symbols() if not hasattr(lib, s)]
+    assert not missing, missing
+
+
+def test_python_binding_types_every_declared_symbol():
+    from deep_attention_visual_odometry_amd import _native
+
+    assert sorted(_native.SIGNATURES) == _declared_symbols()
+
+
+def test_library_is_built_for_gfx950(lib):
+    assert lib.dava_device_arch() == b"gfx950"
+    assert lib.dava_abi_version() == 1
+    blob = open(lib._name, "rb").read()
+    assert b"gfx950" in blob
+
+
+def test_status_strings(lib):
+    assert lib.dava_status_string(0) == b"ok"
+    assert b"invalid" in lib.dava_status_string(1)
+    assert lib.dava_status_string(99) == b"unknown status"
+
+
+def test_invalid_arguments_are_rejected_without_a_device(lib):
+    from deep_attention_visual_odometry_amd import _native as N
+
+    assert lib.dava_ba_solve(None, None, None, None, None, None, None, 0, None) == 1
+    bad = N.DavaScene(4, 1, 16, 0, 3 + 48, None, None)  # one view
+    cfg = N.DavaSolverConfig(1e-4, 0.9, 1e-4, 1e-8, 10, 1000, 1, 0)
+    assert lib.dava_ba_solve(ctypes.byref(bad), ctypes.byref(cfg), None, None, None, None, None, 0, None) == 1
+    wrong_p = N.DavaScene(4, 2, 16, 0, 50, None, None)
+    assert lib.dava_ba_evaluate(ctypes.byref(wrong_p), None, None, None, None, None, None, None) == 1
+    empty = N.DavaScene(0, 2, 16, 0, 3 + 48 + 6, None, None)
+    assert lib.dava_ba_solve(ctypes.byref(empty), ctypes.byref(cfg), None, None, None, None, None, 0, None) == 0
+    assert lib.dava_bfgs_update_inverse_hessian_f32(-1, 3, None, None, None, None, None) == 1
+    assert lib.dava_bfgs_update_inverse_hessian_f64(0, 3, None, None, None, None, None) == 0
+
+
+def test_workspace_size_dense(lib):
+    from deep_attention_visual_odometry_amd import native_ops
+
+    p = 3 + 3 * 256 + 6 * 3 + 5
+    assert native_ops.solve_workspace_bytes(8192, 4, 256, True) == 8192 * p * ((p + 31) // 32 * 32) * 4
+
+
+def test_product_refuses_cpu_tensors():
+    import torch
+
+    from deep_attention_visual_odometry_amd import BFGSSolver, ReprojectionError
+
+    obs = torch.zeros(1, 2, 4, 2)
+    vis = torch.ones(1, 2, 4, dtype=torch.bool)
+    fn = ReprojectionError(obs, vis, 2, 4)
+    with pytest.raises(RuntimeError, match="ROCm device"):
+        BFGSSolver().eval()(torch.zeros(1, 3 + 12 + 6), fn)
+
+
+def test_unpack_matches_reference_layout():
+    import torch
+
+    from deep_attention_visual_odometry_amd import unpack_calibration_parameters
+
+    x = torch.arange(3 + 3 * 5 + 6 * 2, dtype=torch.float32).reshape(1, -1)
+    parts = unpack_calibration_parameters(x, 3, 5)
+    assert parts.intrinsics.shape == (1, 1, 1, 3)
+    assert parts.world_points.shape == (1, 1, 5, 3)
+    assert parts.camera_translations.shape == (1, 2, 1, 3)
+    assert parts.camera_rotations.shape == (1, 2, 1, 3)
+    assert parts.camera_rotations[0, 1, 0, 2].item() == x[0, -1].item()
+    with pytest.raises(ValueError):
+        unpack_calibration_parameters(x[:, :-1], 3, 5)
