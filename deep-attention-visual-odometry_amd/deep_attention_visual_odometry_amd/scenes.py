@@ -10,24 +10,27 @@ Distributions (per problem), in camera 0's frame:
 
 * f = 1/tan(a/2), a ~ U(pi/6, 2pi/3)                 (dataset ``:148-150``)
 * cx, cy ~ clamp(0.2 N(0,1), -0.5, 0.5)               (``:149``)
-* X_xy ~ N(0, 3^2), X_z = 20 + 5 clip(N(0,1), -3, 3)  (``:90-94``, clipped so no
-  point sits on a camera plane)
 * views m >= 1 look at the cloud, like the dataset's look-at construction
   (``:100-133``): centre C_m ~ N(0, 3^2), target (0, 0, 20) + N(0, 1), roll
   ~ N(0, 0.1^2); stored as axis-angle w_m and t_m = -R(w_m) C_m
+* points X_xy ~ N(0, 3^2), X_z = 20 + 5 clip(N(0,1), -2, 2)   (``:90-94``),
+  REJECTION-SAMPLED until every point projects inside |u|, |v| < 0.9 in every
+  view (the dataset's visibility window ``:194-197``)
 * k1 ~ N(0, 1e-2^2), k2 ~ N(0, 1e-3^2), k3 ~ N(0, 1e-4^2), p1, p2 ~ N(0, 1e-3^2)
 * observations: noise-free projection of the truth (fp64, then fp32)
-* visibility: |u| < 1 and |v| < 1 (``:194-197``) or all-true
+* visibility: all ones, or each (m, n) dropped with probability ``drop``
+  (the pair stays in-image, so its residual is finite)
 * initial guess x0 = truth + N(0, 0.01^2) on the pinhole block; the five
   distortion coefficients get 10 % of their own spread
-  (N(0, [1e-3, 1e-4, 1e-5, 1e-4, 1e-4]^2)) -- a 0.01 kick on k3 (spread 1e-4)
-  is 100 sigma and sends k3 r^6 to ~1e2 at the image edge.
+  (N(0, [1e-3, 1e-4, 1e-5, 1e-4, 1e-4]^2)).
 
-Why look-at views: with independent random rotations (no look-at) many
-cameras face away from the cloud, points land near a camera plane, and
-invisible pairs overflow (inf * vis 0 = NaN poisons E in the reference's
-objective too); two-view problems also become so ill-conditioned that the
-reference's own fp32 trajectory changes by 1e-4 under a 1-ulp input nudge.
+Why every point is in-image: the reference objective masks with
+``(residual^2 * vis).sum()``, so an invisible pair whose projection overflows
+at a trial point gives inf * 0 = NaN, and the reference line search (all of
+whose tests are NaN-false) then widens or bisects for its full 1000 trials
+and walks to inf.  With independent random rotations ~20 % of the
+Brown-Conrady problems did exactly that -- in the oracle as well as on the
+GPU.  Look-at views + in-image points keep every residual finite.
 
 Parameter layout: see ``camera_model.layout``.
 """
@@ -71,6 +74,13 @@ def _look_at(forward: np.ndarray, roll: float) -> Rotation:
     return Rotation.from_rotvec([0.0, 0.0, roll]) * align
 
 
+def _pack(f, c, pts, t, w, k) -> np.ndarray:
+    row = [np.array([f, c[0], c[1]]), pts.ravel(), t.ravel(), w.ravel()]
+    if k is not None:
+        row.append(k)
+    return np.concatenate(row)
+
+
 def project_truth(x: np.ndarray, num_views: int, num_points: int, distortion: bool) -> np.ndarray:
     """(M, N, 2) fp64 projection of one parameter vector (no scale normalisation:
     the projection is invariant to it)."""
@@ -102,8 +112,8 @@ def make_scenes(
     distortion: bool = False,
     seed: int = 20251015,
     first_index: int = 0,
-    all_visible: bool = False,
     initial_noise: float = 0.01,
+    drop: float = 0.0,
 ) -> SceneBatch:
     """Problems ``first_index .. first_index + batch - 1`` of the stream ``seed``."""
     if num_views < 2:
@@ -118,8 +128,6 @@ def make_scenes(
         a = np.pi / 6 + (np.pi / 2) * rng.random()
         f = 1.0 / np.tan(a / 2.0)
         c = np.clip(0.2 * rng.standard_normal(2), -0.5, 0.5)
-        xy = 3.0 * rng.standard_normal((num_points, 2))
-        z = 20.0 + 5.0 * np.clip(rng.standard_normal((num_points, 1)), -3.0, 3.0)
         t = np.empty((num_views - 1, 3))
         w = np.empty((num_views - 1, 3))
         for m in range(num_views - 1):
@@ -128,14 +136,23 @@ def make_scenes(
             rot = _look_at(target - centre, 0.1 * rng.standard_normal())
             w[m] = rot.as_rotvec()
             t[m] = -rot.apply(centre)
-        row = [np.array([f, c[0], c[1]]), np.concatenate([xy, z], axis=1).ravel(), t.ravel(), w.ravel()]
-        if distortion:
-            row.append(rng.standard_normal(5) * np.array([1e-2, 1e-3, 1e-4, 1e-3, 1e-3]))
-        x = np.concatenate(row)
+        k = rng.standard_normal(5) * np.array([1e-2, 1e-3, 1e-4, 1e-3, 1e-3]) if distortion else None
+        pts = np.empty((0, 3))
+        for _ in range(1000):
+            cand = np.concatenate([3.0 * rng.standard_normal((2 * num_points, 2)),
+                                   20.0 + 5.0 * np.clip(rng.standard_normal((2 * num_points, 1)), -2.0, 2.0)], axis=1)
+            x = _pack(f, c, cand, t, w, k)
+            uv = project_truth(x, num_views, cand.shape[0], distortion)
+            inside = (np.abs(uv) < 0.9).all(axis=(0, 2))
+            pts = np.concatenate([pts, cand[inside]])
+            if pts.shape[0] >= num_points:
+                break
+        else:
+            raise RuntimeError("could not place points inside every view")
+        x = _pack(f, c, pts[:num_points], t, w, k)
         truth[b] = x
-        uv = project_truth(x, num_views, num_points, distortion)
-        obs[b] = uv
-        vis[b] = True if all_visible else (np.abs(uv[..., 0]) < 1.0) & (np.abs(uv[..., 1]) < 1.0)
+        obs[b] = project_truth(x, num_views, num_points, distortion)
+        vis[b] = True if drop <= 0.0 else rng.random((num_views, num_points)) >= drop
         kick = initial_noise * rng.standard_normal(p)
         if distortion:
             kick[-5:] *= np.array([1e-1, 1e-2, 1e-3, 1e-2, 1e-2])

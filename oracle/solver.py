@@ -157,8 +157,10 @@ def bfgs_solve(
     iterations: int = 1000,
     minimum_step: float = 1e-8,
     record: Optional[SolveRecord] = None,
+    trajectory: Optional[list] = None,
 ) -> torch.Tensor:
-    """Eval-mode ``BFGSSolver.forward`` (``bfgs_solver.py:80-215``)."""
+    """Eval-mode ``BFGSSolver.forward`` (``bfgs_solver.py:80-215``).
+    ``trajectory`` (optional list) receives x after every iteration's step."""
     x = x0.detach()
     shape = x.shape[:-1]
     p = x.size(-1)
@@ -215,6 +217,8 @@ def bfgs_solve(
         step = step.masked_scatter(active.unsqueeze(-1).expand_as(step), s)
         x = x.masked_scatter(active.unsqueeze(-1).expand_as(x), xa + s)
         steps_taken[active] += 1
+        if trajectory is not None:
+            trajectory.append(x.detach().clone())
         still = active & (torch.linalg.vector_norm(step, dim=-1) > minimum_step)
         reason[active & ~still] = STOP_STEP
         active = still

@@ -97,8 +97,10 @@ def closure_for(obs, vis, m, n, batch_mask_full=None):
     return fn
 
 
-def scenes_as_tensors(batch, m, n, seed, dtype):
-    s = make_scenes(batch, m, n, distortion=False, seed=seed)
+def scenes_as_tensors(batch, m, n, seed, dtype, drop=0.1):
+    """Scenes from the product generator; 10 % of (view, point) pairs masked out so the
+    visibility weighting is exercised."""
+    s = make_scenes(batch, m, n, distortion=False, seed=seed, drop=drop)
     return (
         s,
         torch.tensor(s.initial, dtype=dtype),

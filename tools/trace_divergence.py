@@ -1,7 +1,7 @@
 """Diagnostic: find the first BFGS iteration where the fused GPU solve departs
 from the CPU oracle (run on the GPU box).
 
-usage: python tools/trace_divergence.py M N DISTORT B SEED KMAX
+usage: python tools/trace_divergence.py M N DISTORT B SEED KMAX [FIRST_INDEX]
 """
 import os
 import sys
@@ -17,18 +17,21 @@ from oracle import objective, solver  # noqa: E402
 
 def main():
     m, n, dist, b, seed, kmax = (int(a) for a in sys.argv[1:7])
+    first = int(sys.argv[7]) if len(sys.argv) > 7 else 0
     dev = torch.device("cuda", 0)
-    s = make_scenes(b, m, n, distortion=bool(dist), seed=seed)
+    s = make_scenes(b, m, n, distortion=bool(dist), seed=seed, first_index=first)
     x0 = torch.tensor(s.initial)
     obs = torch.tensor(s.observations)
     vis = torch.tensor(s.visibility)
     fn = objective.ReprojectionClosure(obs, vis, m, n, bool(dist))
+    traj = []
+    solver.bfgs_solve(x0, fn, iterations=kmax, error_threshold=-1.0, minimum_step=-1.0, trajectory=traj)
     prev_g = prev_o = x0
     for k in range(1, kmax + 1):
         xg, eg, st = native_ops.ba_solve(x0.to(dev), obs.to(dev), vis.to(dev), m, n, bool(dist), iterations=k,
                                          error_threshold=-1.0, minimum_step=-1.0, want_error=True, want_status=True)
         xg = xg.cpu()
-        xo = solver.bfgs_solve(x0, fn, iterations=k, error_threshold=-1.0, minimum_step=-1.0)
+        xo = traj[k - 1]
         rel = ((xg.double() - xo.double()).norm(dim=-1) / xo.double().norm(dim=-1))
         reli = ((xg[:, :3].double() - xo[:, :3].double()).norm(dim=-1) / xo[:, :3].double().norm(dim=-1))
         eo = objective.reprojection_error(xo.double(), obs.double(), vis, m, n, bool(dist))
