@@ -99,7 +99,14 @@ def main():
 
     distortion = not args.no_distortion
     b = args.batch
-    scenes = make_scenes(b, args.views, args.points, distortion=distortion, seed=args.seed, first_index=rank * b)
+    cache = f"/tmp/dava_scenes_{args.seed}_{rank * b}_{b}_{args.views}_{args.points}_{int(distortion)}.npz"
+    if os.path.exists(cache):  # generation is ~1 ms/problem on the host; cache it for repeated runs
+        z = np.load(cache)
+        scenes = type("S", (), {k: z[k] for k in ("initial", "observations", "visibility")})
+    else:
+        scenes = make_scenes(b, args.views, args.points, distortion=distortion, seed=args.seed,
+                             first_index=rank * b)
+        np.savez(cache, initial=scenes.initial, observations=scenes.observations, visibility=scenes.visibility)
     x0_cpu = torch.tensor(scenes.initial)
     obs_cpu = torch.tensor(scenes.observations)
     vis_cpu = torch.tensor(scenes.visibility)

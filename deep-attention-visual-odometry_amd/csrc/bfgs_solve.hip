@@ -66,8 +66,37 @@ __host__ __device__ inline LdsCarve carve_lds(int M, int N, int Pv) {
   return c;
 }
 
+typedef float f4v __attribute__((ext_vector_type(4)));
+
 __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
 __device__ __forceinline__ void st4(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
+
+#ifndef DAVA_SWEEP_ROWS
+#define DAVA_SWEEP_ROWS 4
+#endif
+#ifndef DAVA_SWEEP_NT
+#define DAVA_SWEEP_NT 0
+#endif
+#ifndef DAVA_DIAG_NO_HBM
+#define DAVA_DIAG_NO_HBM 0
+#endif
+
+// Streaming access to the inverse Hessian: every element is read once and
+// written once per BFGS iteration, never reused by another workgroup.
+__device__ __forceinline__ f4v h_load(const float* p) {
+#if DAVA_SWEEP_NT
+  return __builtin_nontemporal_load(reinterpret_cast<const f4v*>(p));
+#else
+  return *reinterpret_cast<const f4v*>(p);
+#endif
+}
+__device__ __forceinline__ void h_store(float* p, f4v v) {
+#if DAVA_SWEEP_NT
+  __builtin_nontemporal_store(v, reinterpret_cast<f4v*>(p));
+#else
+  *reinterpret_cast<f4v*>(p) = v;
+#endif
+}
 
 // Apply the pending rank-2 term to one element (bfgs_solver.py:298-303 order:
 // ((H + (s_rho_i s_j) c) - s_rho_i yH_j) - Hy_i s_rho_j, no FMA contraction).
@@ -80,18 +109,26 @@ __device__ __forceinline__ float rank2(float h, float sri, float sj, float c, fl
 // One sweep over the dense inverse Hessian of this problem.
 //   H' = Hs + pending,  Hs = stored matrix (or gamma0*I if not materialised)
 //   hy_out[j] = sum_i H'_ij y_i,  hg_out[j] = sum_i H'_ij g_i   (y = g - gp)
-// Writes H' back.  Wave w owns 256-column chunks w, w+4, ...; lane l owns 4
-// consecutive columns, so every global access is a 1 KiB contiguous row piece.
+// Writes H' back.  Column ownership: the ceil(P/4) float4 column groups are
+// split evenly over the 4 waves (wave w owns groups [w*Gw, (w+1)*Gw)), one
+// group per lane per 64-group block, so every wave streams and every global
+// access is a contiguous row piece of up to 1 KiB.  Lane = column means the
+// column sums need no cross-lane reduction.  U rows are loaded before any is
+// consumed to keep U KiB per wave in flight.
 __device__ void dense_sweep(const Layout& L, int Pld, float* __restrict__ H, bool materialized, float gamma0,
                             const float* ps, const float* phy, float prho, float pc, const float* g,
                             const float* gp, float* hy_out, float* hg_out) {
+  constexpr int U = DAVA_SWEEP_ROWS;
   const int P = L.P;
   const int lane = threadIdx.x & (kWave - 1);
   const int wave = threadIdx.x / kWave;
-  const int nchunk = (P + 255) / 256;
-  for (int c = wave; c < nchunk; c += kWaves) {
-    const int j0 = c * 256 + lane * 4;
-    const bool act = j0 < P;
+  const int G = (P + 3) / 4;                      // float4 column groups
+  const int Gw = (G + kWaves - 1) / kWaves;       // groups per wave
+  const int g_end = min(G, (wave + 1) * Gw);
+  for (int gb = wave * Gw; gb < g_end; gb += kWave) {
+    const int grp = gb + lane;
+    const bool act = grp < g_end;
+    const int j0 = grp * 4;
     float sj[4] = {0, 0, 0, 0}, hj[4] = {0, 0, 0, 0}, srj[4] = {0, 0, 0, 0};
     if (act) {
       const float4 a = ld4(ps + j0), b = ld4(phy + j0);
@@ -102,51 +139,40 @@ __device__ void dense_sweep(const Layout& L, int Pld, float* __restrict__ H, boo
     }
     float ay[4] = {0, 0, 0, 0}, ag[4] = {0, 0, 0, 0};
     float* col = H + j0;
-    constexpr int U = 4;  // rows in flight per lane
-    int i = 0;
-    for (; i + U <= P; i += U) {
-      float4 h[U];
-      if (materialized) {
-#pragma unroll
-        for (int u = 0; u < U; ++u) h[u] = act ? ld4(col + (size_t)(i + u) * Pld) : make_float4(0, 0, 0, 0);
-      } else {
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-          const int r = i + u;
-          h[u] = make_float4(r == j0 ? gamma0 : 0.f, r == j0 + 1 ? gamma0 : 0.f, r == j0 + 2 ? gamma0 : 0.f,
-                             r == j0 + 3 ? gamma0 : 0.f);
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int r = i + u;
-        const float gi = g[r], yi = gi - gp[r];
-        const float sri = __fmul_rn(ps[r], prho), hyi = phy[r];
-        float e[4] = {h[u].x, h[u].y, h[u].z, h[u].w};
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          e[k] = rank2(e[k], sri, sj[k], pc, hj[k], hyi, srj[k]);
-          ay[k] += e[k] * yi;
-          ag[k] += e[k] * gi;
-        }
-        if (act) st4(col + (size_t)r * Pld, make_float4(e[0], e[1], e[2], e[3]));
-      }
-    }
-    for (; i < P; ++i) {
-      float4 h = make_float4(0, 0, 0, 0);
-      if (materialized) { if (act) h = ld4(col + (size_t)i * Pld); }
-      else h = make_float4(i == j0 ? gamma0 : 0.f, i == j0 + 1 ? gamma0 : 0.f, i == j0 + 2 ? gamma0 : 0.f,
-                           i == j0 + 3 ? gamma0 : 0.f);
-      const float gi = g[i], yi = gi - gp[i];
-      const float sri = __fmul_rn(ps[i], prho), hyi = phy[i];
-      float e[4] = {h.x, h.y, h.z, h.w};
+    auto row_update = [&](int r, f4v h) {
+      const float gi = g[r], yi = gi - gp[r];
+      const float sri = __fmul_rn(ps[r], prho), hyi = phy[r];
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
-        e[k] = rank2(e[k], sri, sj[k], pc, hj[k], hyi, srj[k]);
-        ay[k] += e[k] * yi;
-        ag[k] += e[k] * gi;
+        h[k] = rank2(h[k], sri, sj[k], pc, hj[k], hyi, srj[k]);
+        ay[k] += h[k] * yi;
+        ag[k] += h[k] * gi;
       }
-      if (act) st4(col + (size_t)i * Pld, make_float4(e[0], e[1], e[2], e[3]));
+#if !DAVA_DIAG_NO_HBM
+      if (act) h_store(col + (size_t)r * Pld, h);
+#endif
+    };
+    auto synth = [&](int r) {  // row r of gamma0 * I restricted to this lane's 4 columns
+      f4v h;
+      h[0] = r == j0 ? gamma0 : 0.f; h[1] = r == j0 + 1 ? gamma0 : 0.f;
+      h[2] = r == j0 + 2 ? gamma0 : 0.f; h[3] = r == j0 + 3 ? gamma0 : 0.f;
+      return h;
+    };
+    int i = 0;
+#if DAVA_DIAG_NO_HBM  // timing-only build: no matrix traffic (results are wrong)
+    materialized = false;
+#endif
+    if (materialized) {
+      for (; i + U <= P; i += U) {
+        f4v h[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) h[u] = act ? h_load(col + (size_t)(i + u) * Pld) : f4v{0, 0, 0, 0};
+#pragma unroll
+        for (int u = 0; u < U; ++u) row_update(i + u, h[u]);
+      }
+      for (; i < P; ++i) row_update(i, act ? h_load(col + (size_t)i * Pld) : f4v{0, 0, 0, 0});
+    } else {
+      for (; i < P; ++i) row_update(i, synth(i));
     }
     if (act) {
       st4(hy_out + j0, make_float4(ay[0], ay[1], ay[2], ay[3]));

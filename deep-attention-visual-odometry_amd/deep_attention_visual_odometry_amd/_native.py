@@ -13,7 +13,7 @@ import threading
 import torch  # noqa: F401  (must be loaded before the library, see above)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "_lib", "libdava_ba.so")
+LIB_PATH = os.environ.get("DAVA_LIB") or os.path.join(_HERE, "_lib", "libdava_ba.so")  # DAVA_LIB: A/B builds
 
 DAVA_OK = 0
 DAVA_HESSIAN_DENSE = 0
