@@ -64,6 +64,17 @@ def dense_algorithmic_bytes(p: int, mn: int, iters: int) -> float:
     return h + 9.0 * mn + 8.0 * p
 
 
+def compact_algorithmic_bytes(p: int, mn: int, iters: int) -> float:
+    """Minimum HBM bytes of the compact-history algorithm for one problem (Pv = P rounded
+    up to 4 floats): iteration k >= 2 reads the k-1 history rows of S and W twice (dots,
+    then the weighted sums) = 16 (k-1) Pv; iterations k = 1 .. K-1 append one S and one W
+    row = 8 Pv; scene and x0 read once, x written once."""
+    pv = (p + 3) // 4 * 4
+    reads = 16.0 * pv * sum(k - 1 for k in range(2, iters))
+    writes = 8.0 * pv * max(iters - 1, 0)
+    return reads + writes + 9.0 * mn + 8.0 * p
+
+
 def cpu_baseline(args, x0, obs, vis, p):
     from oracle import objective, solver
 
@@ -165,7 +176,8 @@ def main():
 
     if rank == 0:
         value = world * b * args.steps / elapsed
-        algo = b * dense_algorithmic_bytes(p, mn, args.iterations) if args.mode == "dense" else None
+        algo = b * (dense_algorithmic_bytes if args.mode == "dense" else compact_algorithmic_bytes)(
+            p, mn, args.iterations)
         roofline = None
         if algo is not None:
             achieved = algo / (launch_ms * 1e-3) / 1e9

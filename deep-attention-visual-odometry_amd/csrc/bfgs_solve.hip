@@ -39,13 +39,14 @@ struct SolveArgs {
   float* hess;
   float c1, c2, thr, min_step;
   int iters, max_trials, strong, mode;
+  int kcap;  // COMPACT: history capacity (entries)
 };
 
 struct LdsCarve {
-  int x, d, g0, g1, s0, s1, hy0, hy1, hg, obs, views, vpart, scratch, vis_bytes_off, total_bytes;
+  int x, d, g0, g1, s0, s1, hy0, hy1, hg, obs, views, vpart, scratch, hcoef, hrho, hc, vis_bytes_off, total_bytes;
 };
 
-__host__ __device__ inline LdsCarve carve_lds(int M, int N, int Pv) {
+__host__ __device__ inline LdsCarve carve_lds(int M, int N, int Pv, int kcap = 0) {
   LdsCarve c;
   int off = 0;
   c.x = off; off += Pv;
@@ -61,6 +62,9 @@ __host__ __device__ inline LdsCarve carve_lds(int M, int N, int Pv) {
   c.views = off; off += round_up(views_floats(M), 4);
   c.vpart = off; off += round_up(vpart_floats(M), 4);
   c.scratch = off; off += 2 * kWaves * 32;
+  c.hcoef = off; off += 4 * kcap;  // COMPACT: per-entry product coefficients
+  c.hrho = off; off += round_up(kcap, 4);
+  c.hc = off; off += round_up(kcap, 4);
   c.vis_bytes_off = off * 4;
   c.total_bytes = c.vis_bytes_off + round_up(M * N, 16);
   return c;
@@ -79,6 +83,12 @@ __device__ __forceinline__ void st4(float* p, float4 v) { *reinterpret_cast<floa
 #endif
 #ifndef DAVA_DIAG_NO_HBM
 #define DAVA_DIAG_NO_HBM 0
+#endif
+#ifndef DAVA_DIAG_NO_SWEEP
+#define DAVA_DIAG_NO_SWEEP 0
+#endif
+#ifndef DAVA_SOLVE_WAVES_PER_EU
+#define DAVA_SOLVE_WAVES_PER_EU 1
 #endif
 
 // Streaming access to the inverse Hessian: every element is read once and
@@ -181,18 +191,93 @@ __device__ void dense_sweep(const Layout& L, int Pld, float* __restrict__ H, boo
   }
 }
 
-__global__ __launch_bounds__(kBlock) void bfgs_ba_solve_kernel(SolveArgs a) {
+// COMPACT mode: the inverse Hessian is never formed.  The exact BFGS history
+//   H_k = gamma0 I + sum_j U_j,   U_j v = c_j rho_j (s_j.v) s_j - rho_j (w_j.v) s_j - rho_j (s_j.v) w_j
+// (w_j = H_{j-1} y_j, the same rank-2 terms the reference adds to its dense H,
+// bfgs_solver.py:263-303) is kept in HBM as rows S[j], W[j] of Pv floats, so
+// a product H v costs 2 passes over 2 nh P floats instead of a P^2 sweep.
+// Pass 1: 4 dots per entry (s.y, w.y, s.g, w.g) -> coefficients in LDS.
+// Pass 2: a = H y and b = H g as coefficient-weighted sums of the rows.
+__device__ void compact_products(int P, int Pv, int nh, const float* __restrict__ S, const float* __restrict__ W,
+                                 float* coef, const float* hrho, const float* hc, float gamma0, const float* g,
+                                 const float* gp, float* a_out, float* b_out) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wave = threadIdx.x / kWave;
+  const int G = (P + 3) / 4;
+  for (int j = wave; j < nh; j += kWaves) {
+    const float* sr = S + (size_t)j * Pv;
+    const float* wr = W + (size_t)j * Pv;
+    float sy = 0.f, wy = 0.f, sg = 0.f, wg = 0.f;
+    for (int q = lane; q < G; q += kWave) {
+      const f4v s4 = *reinterpret_cast<const f4v*>(sr + 4 * q);
+      const f4v w4 = *reinterpret_cast<const f4v*>(wr + 4 * q);
+      const float4 g4 = ld4(g + 4 * q), p4 = ld4(gp + 4 * q);
+      const float y0 = g4.x - p4.x, y1 = g4.y - p4.y, y2 = g4.z - p4.z, y3 = g4.w - p4.w;
+      sy += s4[0] * y0 + s4[1] * y1 + s4[2] * y2 + s4[3] * y3;
+      wy += w4[0] * y0 + w4[1] * y1 + w4[2] * y2 + w4[3] * y3;
+      sg += s4[0] * g4.x + s4[1] * g4.y + s4[2] * g4.z + s4[3] * g4.w;
+      wg += w4[0] * g4.x + w4[1] * g4.y + w4[2] * g4.z + w4[3] * g4.w;
+    }
+    sy = wave_sum(sy); wy = wave_sum(wy); sg = wave_sum(sg); wg = wave_sum(wg);
+    if (lane == 0) {
+      const float rho = hrho[j], cr = hc[j] * rho;
+      coef[4 * j + 0] = cr * sy - rho * wy;
+      coef[4 * j + 1] = -rho * sy;
+      coef[4 * j + 2] = cr * sg - rho * wg;
+      coef[4 * j + 3] = -rho * sg;
+    }
+  }
+  __syncthreads();
+  for (int q = threadIdx.x; q < G; q += kBlock) {
+    const float4 g4 = ld4(g + 4 * q), p4 = ld4(gp + 4 * q);
+    f4v y4 = {g4.x - p4.x, g4.y - p4.y, g4.z - p4.z, g4.w - p4.w};
+    f4v gg = {g4.x, g4.y, g4.z, g4.w};
+    f4v a4 = gamma0 * y4, b4 = gamma0 * gg;
+    const float* sr = S + 4 * q;
+    const float* wr = W + 4 * q;
+    int j = 0;
+    for (; j + 4 <= nh; j += 4) {
+      f4v s4[4], w4[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        s4[u] = *reinterpret_cast<const f4v*>(sr + (size_t)(j + u) * Pv);
+        w4[u] = *reinterpret_cast<const f4v*>(wr + (size_t)(j + u) * Pv);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const float4 cf = ld4(coef + 4 * (j + u));
+        a4 += cf.x * s4[u] + cf.y * w4[u];
+        b4 += cf.z * s4[u] + cf.w * w4[u];
+      }
+    }
+    for (; j < nh; ++j) {
+      const f4v s4 = *reinterpret_cast<const f4v*>(sr + (size_t)j * Pv);
+      const f4v w4 = *reinterpret_cast<const f4v*>(wr + (size_t)j * Pv);
+      const float4 cf = ld4(coef + 4 * j);
+      a4 += cf.x * s4 + cf.y * w4;
+      b4 += cf.z * s4 + cf.w * w4;
+    }
+    st4(a_out + 4 * q, make_float4(a4[0], a4[1], a4[2], a4[3]));
+    st4(b_out + 4 * q, make_float4(b4[0], b4[1], b4[2], b4[3]));
+  }
+}
+
+template <int MODE>
+__global__ __launch_bounds__(kBlock, DAVA_SOLVE_WAVES_PER_EU) void bfgs_ba_solve_kernel(SolveArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const Layout L = a.L;
   const int P = L.P, M = L.M, N = L.N;
   const int Pv = a.Pv;
   const int b = blockIdx.x;
   const int tid = threadIdx.x;
-  const LdsCarve cv = carve_lds(M, N, Pv);
+  const LdsCarve cv = carve_lds(M, N, Pv, MODE == DAVA_HESSIAN_COMPACT ? a.kcap : 0);
   float* x = lds + cv.x;
   float* d = lds + cv.d;
   float* g = lds + cv.g0;
   float* gp = lds + cv.g1;
+  float* hcoef = lds + cv.hcoef;
+  float* hrho = lds + cv.hrho;
+  float* hc = lds + cv.hc;
   float* s_cur = lds + cv.s0;
   float* s_pend = lds + cv.s1;
   float* hy_new = lds + cv.hy0;
@@ -217,7 +302,15 @@ __global__ __launch_bounds__(kBlock) void bfgs_ba_solve_kernel(SolveArgs a) {
   for (int i = tid; i < MN; i += kBlock) vis[i] = vb[i] ? 1 : 0;
   __syncthreads();
 
-  float* H = a.hess ? a.hess + (size_t)b * P * a.Pld : nullptr;
+  float* H = nullptr;   // DENSE: this problem's P x Pld inverse Hessian
+  float* SH = nullptr;  // COMPACT: history rows S[kcap][Pv], W[kcap][Pv]
+  float* WH = nullptr;
+  if (MODE == DAVA_HESSIAN_DENSE) {
+    H = a.hess ? a.hess + (size_t)b * P * a.Pld : nullptr;
+  } else if (a.hess) {
+    SH = a.hess + (size_t)b * 2 * a.kcap * Pv;
+    WH = SH + (size_t)a.kcap * Pv;
+  }
   int buf = 0;
   bool materialized = false;
   float gamma0 = 1.f, pend_rho = 0.f, pend_c = 1.f;
@@ -257,8 +350,16 @@ __global__ __launch_bounds__(kBlock) void bfgs_ba_solve_kernel(SolveArgs a) {
         }
         // (no barrier needed: each thread reads back only its own hy_new / hg below)
       } else {
-        dense_sweep(L, a.Pld, H, materialized, gamma0, s_pend, hy_pend, pend_rho, pend_c, g, gp, hy_new, hg);
-        materialized = true;
+#if DAVA_DIAG_NO_SWEEP  // timing-only build: H stays gamma0 I (results are wrong)
+        for (int i = tid; i < P; i += kBlock) { hy_new[i] = gamma0 * (g[i] - gp[i]); hg[i] = gamma0 * g[i]; }
+#else
+        if constexpr (MODE == DAVA_HESSIAN_DENSE) {
+          dense_sweep(L, a.Pld, H, materialized, gamma0, s_pend, hy_pend, pend_rho, pend_c, g, gp, hy_new, hg);
+          materialized = true;
+        } else {
+          compact_products(P, Pv, k - 1, SH, WH, hcoef, hrho, hc, gamma0, g, gp, hy_new, hg);
+        }
+#endif
         __syncthreads();
         for (int i = tid; i < P; i += kBlock) {
           const float gi = g[i], yi = gi - gp[i], si = s_cur[i], hi = hy_new[i];
@@ -276,11 +377,19 @@ __global__ __launch_bounds__(kBlock) void bfgs_ba_solve_kernel(SolveArgs a) {
         const float sri = s_cur[i] * rho;
         d[i] = -1.0f * (hg[i] + sri * (c * sg) - sri * hyg - hy_new[i] * rsg);
       }
-      // the new update becomes the pending one; recycle the old buffers
-      { float* t = s_pend; s_pend = s_cur; s_cur = t; }
-      { float* t = hy_pend; hy_pend = hy_new; hy_new = t; }
-      pend_rho = rho;
-      pend_c = c;
+      if constexpr (MODE == DAVA_HESSIAN_DENSE) {
+        // the new update becomes the pending one; recycle the old buffers
+        { float* t = s_pend; s_pend = s_cur; s_cur = t; }
+        { float* t = hy_pend; hy_pend = hy_new; hy_new = t; }
+        pend_rho = rho;
+        pend_c = c;
+      } else if (k - 1 < a.kcap) {
+        // append U_k = (s, H y, rho, c) to the history (entry k-1)
+        float* sr = SH + (size_t)(k - 1) * Pv;
+        float* wr = WH + (size_t)(k - 1) * Pv;
+        for (int i = tid; i < Pv; i += kBlock) { sr[i] = s_cur[i]; wr[i] = hy_new[i]; }
+        if (tid == 0) { hrho[k - 1] = rho; hc[k - 1] = c; }
+      }
       __syncthreads();
     }
 
@@ -425,8 +534,16 @@ static size_t dense_hessian_bytes(const DavaScene* s) {
   return (size_t)s->batch * (size_t)P * (size_t)round_up(P, 32) * sizeof(float);
 }
 
-static int lds_bytes_for(const DavaScene* s) {
-  return carve_lds(s->num_views, s->num_points, round_up(s->num_parameters, 4)).total_bytes;
+static int lds_bytes_for(const DavaScene* s, int kcap = 0) {
+  return carve_lds(s->num_views, s->num_points, round_up(s->num_parameters, 4), kcap).total_bytes;
+}
+
+// history entries the COMPACT mode needs: one per iteration k = 1 .. iterations-1
+static int compact_capacity(const DavaSolverConfig* c) { return c->iterations > 1 ? c->iterations - 1 : 1; }
+constexpr int kMaxCompactEntries = 1024;
+
+static size_t compact_history_bytes(const DavaScene* s, const DavaSolverConfig* c) {
+  return (size_t)s->batch * 2 * (size_t)compact_capacity(c) * (size_t)round_up(s->num_parameters, 4) * sizeof(float);
 }
 
 constexpr int kMaxLds = 160 * 1024;
@@ -438,6 +555,7 @@ using namespace dava;
 extern "C" size_t dava_ba_solve_workspace_bytes(const DavaScene* scene, const DavaSolverConfig* config) {
   if (check_scene(scene, false) != DAVA_OK || !config) return 0;
   if (config->hessian_mode == DAVA_HESSIAN_DENSE) return dense_hessian_bytes(scene);
+  if (config->hessian_mode == DAVA_HESSIAN_COMPACT) return compact_history_bytes(scene, config);
   return 0;
 }
 
@@ -447,13 +565,17 @@ extern "C" int dava_ba_solve(const DavaScene* scene, const DavaSolverConfig* con
   int st = check_scene(scene);
   if (st != DAVA_OK) return st;
   if (!config || config->iterations < 0 || config->max_line_search_trials < 0) return DAVA_ERR_INVALID_ARGUMENT;
-  if (config->hessian_mode != DAVA_HESSIAN_DENSE) return DAVA_ERR_UNSUPPORTED;
+  const int mode = config->hessian_mode;
+  if (mode != DAVA_HESSIAN_DENSE && mode != DAVA_HESSIAN_COMPACT) return DAVA_ERR_INVALID_ARGUMENT;
   if (scene->batch == 0) return DAVA_OK;
   if (!x0 || !x_out) return DAVA_ERR_INVALID_ARGUMENT;
-  const int lds = lds_bytes_for(scene);
+  const int kcap = mode == DAVA_HESSIAN_COMPACT ? compact_capacity(config) : 0;
+  if (kcap > kMaxCompactEntries) return DAVA_ERR_UNSUPPORTED;
+  const int lds = lds_bytes_for(scene, kcap);
   if (lds > kMaxLds) return DAVA_ERR_UNSUPPORTED;
-  const size_t need = dense_hessian_bytes(scene);
-  if (config->iterations > 2 && (!workspace || workspace_bytes < need)) return DAVA_ERR_WORKSPACE;
+  const size_t need = mode == DAVA_HESSIAN_DENSE ? dense_hessian_bytes(scene) : compact_history_bytes(scene, config);
+  const bool uses_ws = mode == DAVA_HESSIAN_DENSE ? config->iterations > 2 : config->iterations > 1;
+  if (uses_ws && (!workspace || workspace_bytes < need)) return DAVA_ERR_WORKSPACE;
   SolveArgs a;
   a.L = Layout{scene->num_views, scene->num_points, scene->num_parameters, scene->distortion ? 1 : 0};
   a.B = scene->batch;
@@ -473,12 +595,20 @@ extern "C" int dava_ba_solve(const DavaScene* scene, const DavaSolverConfig* con
   a.iters = config->iterations;
   a.max_trials = config->max_line_search_trials;
   a.strong = config->strong_wolfe;
-  a.mode = config->hessian_mode;
+  a.mode = mode;
+  a.kcap = kcap;
   hipStream_t s = static_cast<hipStream_t>(stream);
-  if (lds > 64 * 1024)
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(bfgs_ba_solve_kernel),
-                        hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-  hipLaunchKernelGGL(bfgs_ba_solve_kernel, dim3(scene->batch), dim3(kBlock), lds, s, a);
+  if (mode == DAVA_HESSIAN_DENSE) {
+    if (lds > 64 * 1024)
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(bfgs_ba_solve_kernel<DAVA_HESSIAN_DENSE>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    hipLaunchKernelGGL(bfgs_ba_solve_kernel<DAVA_HESSIAN_DENSE>, dim3(scene->batch), dim3(kBlock), lds, s, a);
+  } else {
+    if (lds > 64 * 1024)
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(bfgs_ba_solve_kernel<DAVA_HESSIAN_COMPACT>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    hipLaunchKernelGGL(bfgs_ba_solve_kernel<DAVA_HESSIAN_COMPACT>, dim3(scene->batch), dim3(kBlock), lds, s, a);
+  }
   return hipGetLastError() == hipSuccess ? DAVA_OK : DAVA_ERR_LAUNCH;
 }
 
