@@ -46,7 +46,7 @@ def parse():
     p.add_argument("--points", type=int, default=256)
     p.add_argument("--no-distortion", action="store_true")
     p.add_argument("--iterations", type=int, default=100)
-    p.add_argument("--mode", choices=["dense", "compact"], default="dense")
+    p.add_argument("--mode", choices=["dense", "compact"], default="compact")
     p.add_argument("--seed", type=int, default=20251015 + 3000)
     p.add_argument("--cpu-sample", type=int, default=12, help="problems timed on the CPU oracle (0 = skip)")
     p.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "pmc_traffic.json"))
@@ -66,11 +66,13 @@ def dense_algorithmic_bytes(p: int, mn: int, iters: int) -> float:
 
 def compact_algorithmic_bytes(p: int, mn: int, iters: int) -> float:
     """Minimum HBM bytes of the compact-history algorithm for one problem (Pv = P rounded
-    up to 4 floats): iteration k >= 2 reads the k-1 history rows of S and W twice (dots,
-    then the weighted sums) = 16 (k-1) Pv; iterations k = 1 .. K-1 append one S and one W
-    row = 8 Pv; scene and x0 read once, x written once."""
+    up to 4 floats): iteration k >= 2 reads the k-1 history rows of S and W -- once
+    (8 (k-1) Pv) on the fused single-pass path used for P <= 1024, twice (dots, then the
+    weighted sums: 16 (k-1) Pv) on the two-pass path for larger P; iterations k = 1 .. K-1
+    append one S and one W row = 8 Pv; scene and x0 read once, x written once."""
     pv = (p + 3) // 4 * 4
-    reads = 16.0 * pv * sum(k - 1 for k in range(2, iters))
+    per_entry = 8.0 if (p + 3) // 4 <= 256 else 16.0
+    reads = per_entry * pv * sum(k - 1 for k in range(2, iters))
     writes = 8.0 * pv * max(iters - 1, 0)
     return reads + writes + 9.0 * mn + 8.0 * p
 

@@ -88,7 +88,7 @@ __device__ __forceinline__ void st4(float* p, float4 v) { *reinterpret_cast<floa
 #define DAVA_DIAG_NO_SWEEP 0
 #endif
 #ifndef DAVA_SOLVE_WAVES_PER_EU
-#define DAVA_SOLVE_WAVES_PER_EU 1
+#define DAVA_SOLVE_WAVES_PER_EU 2  // <= 256 VGPRs: two 4-wave workgroups per CU
 #endif
 
 // Streaming access to the inverse Hessian: every element is read once and
@@ -262,6 +262,120 @@ __device__ void compact_products(int P, int Pv, int nh, const float* __restrict_
   }
 }
 
+// COMPACT mode, single pass (P <= 1024, i.e. at most GM <= 4 float4 groups per lane):
+// the coefficients of entry j depend only on entry j's own dots, so one wave
+// loads the two rows of an entry into registers, reduces its 4 dots in-wave
+// (no barrier), and immediately accumulates the entry's contribution to
+// H y and H g -- every history row crosses HBM once per iteration.  Entries
+// are dealt round-robin to the 4 waves; the per-wave partial sums are then
+// added in a fixed tree ((w0 + w2) + (w1 + w3)) through 4 spare LDS vectors,
+// so the result is deterministic.  a_out / b_out / spare0..3 are Pv-float LDS vectors.
+template <int GM>
+__device__ void compact_products_fused(int P, int Pv, int nh, const float* __restrict__ S,
+                                       const float* __restrict__ W, const float* hrho, const float* hc,
+                                       float gamma0, const float* g, const float* gp, float* a_out, float* b_out,
+                                       float* spare0, float* spare1, float* spare2, float* spare3) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wave = threadIdx.x / kWave;
+  const int G = (P + 3) / 4;
+  f4v pa[GM], pb[GM];
+  bool ok[GM];
+#pragma unroll
+  for (int m = 0; m < GM; ++m) {
+    ok[m] = lane + kWave * m < G;
+    pa[m] = f4v{0, 0, 0, 0};
+    pb[m] = f4v{0, 0, 0, 0};
+  }
+  // y and g stay in LDS (re-read per entry: cheap ds_read_b128, saves 8 GM VGPRs)
+  auto gvec = [&](int m) {
+    const float4 t = ld4(g + 4 * (lane + kWave * m));
+    return f4v{t.x, t.y, t.z, t.w};
+  };
+  auto yvec = [&](int m) {
+    const int q = lane + kWave * m;
+    const float4 t = ld4(g + 4 * q), u = ld4(gp + 4 * q);
+    return f4v{t.x - u.x, t.y - u.y, t.z - u.z, t.w - u.w};
+  };
+  auto consume = [&](int j, const f4v (&s4)[GM], const f4v (&w4)[GM]) {
+    float sy = 0.f, wy = 0.f, sg = 0.f, wg = 0.f;
+#pragma unroll
+    for (int m = 0; m < GM; ++m) {
+      const f4v y = yvec(m), gm = gvec(m);
+      const f4v a = s4[m] * y, b = w4[m] * y, c = s4[m] * gm, e = w4[m] * gm;
+      sy += (a[0] + a[1]) + (a[2] + a[3]);
+      wy += (b[0] + b[1]) + (b[2] + b[3]);
+      sg += (c[0] + c[1]) + (c[2] + c[3]);
+      wg += (e[0] + e[1]) + (e[2] + e[3]);
+    }
+    sy = wave_sum(sy); wy = wave_sum(wy); sg = wave_sum(sg); wg = wave_sum(wg);
+    const float rho = hrho[j], cr = hc[j] * rho;
+    const float ay = cr * sy - rho * wy, by = -rho * sy, ag = cr * sg - rho * wg, bg = -rho * sg;
+#pragma unroll
+    for (int m = 0; m < GM; ++m) {
+      pa[m] += ay * s4[m] + by * w4[m];
+      pb[m] += ag * s4[m] + bg * w4[m];
+    }
+  };
+  auto load = [&](int j, f4v (&s4)[GM], f4v (&w4)[GM]) {
+    const float* sr = S + (size_t)j * Pv;
+    const float* wr = W + (size_t)j * Pv;
+#pragma unroll
+    for (int m = 0; m < GM; ++m) {
+      const int q = lane + kWave * m;
+      s4[m] = ok[m] ? *reinterpret_cast<const f4v*>(sr + 4 * q) : f4v{0, 0, 0, 0};
+      w4[m] = ok[m] ? *reinterpret_cast<const f4v*>(wr + 4 * q) : f4v{0, 0, 0, 0};
+    }
+  };
+  int j = wave;
+  for (; j + kWaves < nh; j += 2 * kWaves) {  // two entries in flight per wave
+    f4v s0[GM], w0[GM], s1[GM], w1[GM];
+    load(j, s0, w0);
+    load(j + kWaves, s1, w1);
+    consume(j, s0, w0);
+    consume(j + kWaves, s1, w1);
+  }
+  if (j < nh) {
+    f4v s0[GM], w0[GM];
+    load(j, s0, w0);
+    consume(j, s0, w0);
+  }
+  // deterministic cross-wave sum: ((w0 + w2) + (w1 + w3)) + gamma0 * (y | g)
+  auto put = [&](float* A, float* B) {
+#pragma unroll
+    for (int m = 0; m < GM; ++m)
+      if (ok[m]) {
+        const int q = lane + kWave * m;
+        *reinterpret_cast<f4v*>(A + 4 * q) = pa[m];
+        *reinterpret_cast<f4v*>(B + 4 * q) = pb[m];
+      }
+  };
+  auto add = [&](const float* A, const float* B) {
+#pragma unroll
+    for (int m = 0; m < GM; ++m)
+      if (ok[m]) {
+        const int q = lane + kWave * m;
+        pa[m] += *reinterpret_cast<const f4v*>(A + 4 * q);
+        pb[m] += *reinterpret_cast<const f4v*>(B + 4 * q);
+      }
+  };
+  if (wave == 2) put(spare0, spare1);
+  if (wave == 3) put(spare2, spare3);
+  __syncthreads();
+  if (wave == 0) add(spare0, spare1);
+  if (wave == 1) { add(spare2, spare3); put(spare2, spare3); }
+  __syncthreads();
+  if (wave == 0) {
+    add(spare2, spare3);
+#pragma unroll
+    for (int m = 0; m < GM; ++m)
+      if (ok[m]) {
+        pa[m] += gamma0 * yvec(m);
+        pb[m] += gamma0 * gvec(m);
+      }
+    put(a_out, b_out);
+  }
+}
+
 template <int MODE>
 __global__ __launch_bounds__(kBlock, DAVA_SOLVE_WAVES_PER_EU) void bfgs_ba_solve_kernel(SolveArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -357,6 +471,14 @@ __global__ __launch_bounds__(kBlock, DAVA_SOLVE_WAVES_PER_EU) void bfgs_ba_solve
           dense_sweep(L, a.Pld, H, materialized, gamma0, s_pend, hy_pend, pend_rho, pend_c, g, gp, hy_new, hg);
           materialized = true;
         } else {
+#ifndef DAVA_COMPACT_TWO_PASS
+          const int GM = ((P + 3) / 4 + kWave - 1) / kWave;
+          if (GM <= 1) compact_products_fused<1>(P, Pv, k - 1, SH, WH, hrho, hc, gamma0, g, gp, hy_new, hg, s_pend, hy_pend, d, hg);
+          else if (GM == 2) compact_products_fused<2>(P, Pv, k - 1, SH, WH, hrho, hc, gamma0, g, gp, hy_new, hg, s_pend, hy_pend, d, hg);
+          else if (GM == 3) compact_products_fused<3>(P, Pv, k - 1, SH, WH, hrho, hc, gamma0, g, gp, hy_new, hg, s_pend, hy_pend, d, hg);
+          else if (GM == 4) compact_products_fused<4>(P, Pv, k - 1, SH, WH, hrho, hc, gamma0, g, gp, hy_new, hg, s_pend, hy_pend, d, hg);
+          else
+#endif
           compact_products(P, Pv, k - 1, SH, WH, hcoef, hrho, hc, gamma0, g, gp, hy_new, hg);
         }
 #endif
