@@ -109,16 +109,18 @@ def main():
 
     from deep_attention_visual_odometry_amd import make_scenes, native_ops
     from deep_attention_visual_odometry_amd import _native
+    from deep_attention_visual_odometry_amd.sharding import gather_rows, shard_range
 
     distortion = not args.no_distortion
     b = args.batch
-    cache = f"/tmp/dava_scenes_{args.seed}_{rank * b}_{b}_{args.views}_{args.points}_{int(distortion)}.npz"
+    first = shard_range(world * b, world, rank).start  # this rank's slab of the global batch
+    cache = f"/tmp/dava_scenes_{args.seed}_{first}_{b}_{args.views}_{args.points}_{int(distortion)}.npz"
     if os.path.exists(cache):  # generation is ~1 ms/problem on the host; cache it for repeated runs
         z = np.load(cache)
         scenes = type("S", (), {k: z[k] for k in ("initial", "observations", "visibility")})
     else:
         scenes = make_scenes(b, args.views, args.points, distortion=distortion, seed=args.seed,
-                             first_index=rank * b)
+                             first_index=first)
         np.savez(cache, initial=scenes.initial, observations=scenes.observations, visibility=scenes.visibility)
     x0_cpu = torch.tensor(scenes.initial)
     obs_cpu = torch.tensor(scenes.observations)
@@ -131,7 +133,6 @@ def main():
     mode = _native.DAVA_HESSIAN_DENSE if args.mode == "dense" else _native.DAVA_HESSIAN_COMPACT
     ws_bytes = native_ops.solve_workspace_bytes(b, args.views, args.points, distortion, mode, args.iterations)
     workspace = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
-    gathered = torch.empty((world * b, p), dtype=torch.float32, device=dev) if world > 1 else None
     stream = torch.cuda.current_stream(dev)
 
     kernel_ms = []
@@ -147,8 +148,9 @@ def main():
         if timed:
             e1.record(stream)
             kernel_ms.append((e0, e1))
-        if world > 1:
-            dist.all_gather_into_tensor(gathered, x)
+        if world > 1:  # the one collective: converged parameters + status of every problem
+            gather_rows(x, world * b)
+            gather_rows(status, world * b)
         return x, status
 
     for _ in range(args.warmup):

@@ -43,7 +43,7 @@ class BFGSSolver(Module):
         return_second_last: bool = False,
         training_iterations: int = None,
         training_error_threshold: float = None,
-        hessian_mode: str = "dense",
+        hessian_mode: str = "auto",
     ):
         super().__init__()
         self.sufficient_decrease = float(sufficient_decrease)
@@ -57,8 +57,8 @@ class BFGSSolver(Module):
         self.training_error_threshold = (
             float(training_error_threshold) if training_error_threshold is not None else self.error_threshold
         )
-        if hessian_mode not in ("dense", "compact"):
-            raise ValueError("hessian_mode must be 'dense' or 'compact'")
+        if hessian_mode not in ("auto", "dense", "compact"):
+            raise ValueError("hessian_mode must be 'auto', 'dense' or 'compact'")
         self.hessian_mode = hessian_mode
         self.last_status: Optional[torch.Tensor] = None
 
@@ -96,7 +96,7 @@ class BFGSSolver(Module):
         x0 = parameters.reshape(-1, parameters.size(-1))
         if x0.dtype != torch.float32:
             raise TypeError("the fused BA solver computes in float32")
-        mode = _native.DAVA_HESSIAN_DENSE if self.hessian_mode == "dense" else _native.DAVA_HESSIAN_COMPACT
+        mode = self._resolve_mode(num_iterations, x0.size(-1))
         x, _, status = native_ops.ba_solve(
             x0, fn.observations.reshape(-1, fn.num_views, fn.num_points, 2),
             fn.visibility.reshape(-1, fn.num_views, fn.num_points), fn.num_views, fn.num_points, fn.distortion,
@@ -105,6 +105,23 @@ class BFGSSolver(Module):
             hessian_mode=mode, want_status=True)
         self.last_status = status
         return x.reshape(parameters.shape)
+
+    MAX_COMPACT_ENTRIES = 1024  # kMaxCompactEntries in csrc/bfgs_solve.hip
+
+    def _resolve_mode(self, num_iterations: int, p: int) -> int:
+        """'auto': the compact history (same math, O(k P) bytes per iteration) unless it would
+        need more than 1024 entries or hold more than 4x the bytes of a dense P x P matrix."""
+        if self.hessian_mode == "dense":
+            return _native.DAVA_HESSIAN_DENSE
+        entries = max(num_iterations - 1, 1)
+        fits = entries <= self.MAX_COMPACT_ENTRIES
+        if self.hessian_mode == "compact":
+            if not fits:
+                raise ValueError(f"compact mode supports at most {self.MAX_COMPACT_ENTRIES + 1} iterations")
+            return _native.DAVA_HESSIAN_COMPACT
+        pv = (p + 3) // 4 * 4
+        small = 2 * entries * pv <= 4 * p * ((p + 31) // 32 * 32)
+        return _native.DAVA_HESSIAN_COMPACT if fits and small else _native.DAVA_HESSIAN_DENSE
 
     def _generic(self, parameters, error_function, error_threshold, num_iterations):
         batch_dimensions = parameters.shape[:-1]
