@@ -431,10 +431,19 @@ __global__ __launch_bounds__(kBlock, DAVA_SOLVE_WAVES_PER_EU) void bfgs_ba_solve
   int steps = 0, reason = DAVA_STOP_ITERATIONS, evals = 0, trials = 0;
   float E = 0.f, unused = 0.f;
 
+  // When the line search accepts the step it evaluated last, that trial (which also
+  // formed the full gradient) IS the evaluation at x_{k+1} = x_k + alpha d: same point,
+  // bit for bit, so the next iteration's objective + gradient are taken from it.
+  bool have_next = false;
+  float E_next = 0.f;
   for (int k = 0; k < a.iters; ++k) {
-    { float* t = g; g = gp; gp = t; }  // gp <- previous gradient
-    ba_eval<true, false, false>(L, x, nullptr, 0.f, obs, vis, g, views, vpart, scratch, buf, E, unused);
-    ++evals;
+    { float* t = g; g = gp; gp = t; }  // gp <- previous gradient; g <- (trial) gradient buffer
+    if (have_next) {
+      E = E_next;
+    } else {
+      ba_eval<true, false, false>(L, x, nullptr, 0.f, obs, vis, g, views, vpart, scratch, buf, E, unused);
+      ++evals;
+    }
     if (!(E > a.thr)) { reason = DAVA_STOP_ERROR; break; }
 
     if (k == 0) {
@@ -524,7 +533,9 @@ __global__ __launch_bounds__(kBlock, DAVA_SOLVE_WAVES_PER_EU) void bfgs_ba_solve
       dphi0 = r[0];
     }
     float a_lo = 0.f, a_hi = 0.f, al = 1.f, f_lo = E, f_hi = E, fa = E, dfa = dphi0;
-    bool widen = true, zoom = false;
+    float last_al = 0.f, last_fa = 0.f;
+    bool widen = true, zoom = false, evaluated = false;
+    // trial gradients go into gp's buffer (g_prev is dead once d is formed)
     const float lim = (-a.c2) * dphi0;
     for (int t = 0; t < a.max_trials; ++t) {
       if (!(widen || zoom)) break;
@@ -532,9 +543,12 @@ __global__ __launch_bounds__(kBlock, DAVA_SOLVE_WAVES_PER_EU) void bfgs_ba_solve
         if (widen) { a_hi = al; f_hi = fa; al = 2.0f * al; }
         if (zoom) al = 0.5f * (a_lo + a_hi);
       }
-      ba_eval<false, true, true>(L, x, d, al, obs, vis, nullptr, views, vpart, scratch, buf, fa, dfa);
+      ba_eval<true, true, true>(L, x, d, al, obs, vis, gp, views, vpart, scratch, buf, fa, dfa);
       ++evals;
       ++trials;
+      evaluated = true;
+      last_al = al;
+      last_fa = fa;
       bool fail = fa > E + (a.c1 * al) * dphi0;
       if (zoom) fail = fail || (fa >= f_lo);
       if (t > 0 && widen) fail = fail || (fa >= f_hi);
@@ -561,6 +575,8 @@ __global__ __launch_bounds__(kBlock, DAVA_SOLVE_WAVES_PER_EU) void bfgs_ba_solve
       if (a_lo == a_hi) zoom = false;
     }
     const float alpha = a_hi;
+    have_next = evaluated && last_al == alpha;
+    E_next = last_fa;
 
     // ---- take the step (bfgs_solver.py:191-199) and test its length (:203-207) ----
     {

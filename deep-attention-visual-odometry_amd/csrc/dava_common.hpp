@@ -28,6 +28,26 @@ __device__ __forceinline__ T wave_sum(T v) {
   return v;
 }
 
+template <int CTRL>
+__device__ __forceinline__ float dpp_mov(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, true));
+}
+
+// fp32 all-lanes wave sum entirely in registers (gfx950): DPP butterflies inside each
+// 16-lane row, then v_permlane16_swap / v_permlane32_swap across rows.  12 VALU ops;
+// the __shfl_xor form costs an LDS round trip (ds_bpermute) plus index math per step.
+template <>
+__device__ __forceinline__ float wave_sum<float>(float v) {
+  v += dpp_mov<0xB1>(v);   // quad_perm [1,0,3,2]: xor 1
+  v += dpp_mov<0x4E>(v);   // quad_perm [2,3,0,1]: xor 2
+  v += dpp_mov<0x141>(v);  // row_half_mirror: xor 4 on quad-uniform data
+  v += dpp_mov<0x140>(v);  // row_mirror: xor 8 on 8-lane-uniform data
+  const auto p = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = __uint_as_float(p[0]) + __uint_as_float(p[1]);  // xor 16
+  const auto q = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(q[0]) + __uint_as_float(q[1]);  // xor 32
+}
+
 // Deterministic block-wide sum of R values: wave butterflies, then the 4 wave
 // partials are added in a fixed order by every thread, so all threads hold
 // bit-identical results (the solver's control flow depends on them being
