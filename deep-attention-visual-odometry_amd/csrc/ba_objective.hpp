@@ -266,7 +266,7 @@ __device__ void ba_eval(const Layout& L, const float* x, const float* d, float a
         vv = vb + in.cy;
       }
       const int pair = m * N + n;
-      const float wgt = (float)vis[pair];
+      const float wgt = vis[pair] ? 1.0f : 0.0f;
       const float ru = u - obs[2 * pair], rv = vv - obs[2 * pair + 1];
       e_loc += (ru * ru + rv * rv) * wgt;
       if constexpr (SLOPE) {

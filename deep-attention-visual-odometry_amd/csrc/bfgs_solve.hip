@@ -23,6 +23,8 @@
 //    never stored (the first sweep synthesises it).
 //  * the line search runs in-kernel; trial slopes come from forward-mode
 //    (JVP) derivatives, gradients at accepted points from reverse mode.
+#include <cstdlib>
+
 #include "ba_objective.hpp"
 
 namespace dava {
@@ -39,26 +41,34 @@ struct SolveArgs {
   float* hess;
   float c1, c2, thr, min_step;
   int iters, max_trials, strong, mode;
-  int kcap;  // COMPACT: history capacity (entries)
+  int kcap;       // COMPACT: history capacity (entries)
+  float* vecs;    // GV mode: B x kVectors x Pv floats (else unused)
 };
 
 struct LdsCarve {
   int x, d, g0, g1, s0, s1, hy0, hy1, hg, obs, views, vpart, scratch, hcoef, hrho, hc, vis_bytes_off, total_bytes;
 };
 
-__host__ __device__ inline LdsCarve carve_lds(int M, int N, int Pv, int kcap = 0) {
+constexpr int kVectors = 9;  // x d g g_prev s s_pend Hy Hy_pend Hg
+
+// LDS image of one problem.  In global-vector (GV) mode -- large P, where the O(P)
+// vectors cannot live on-chip -- the nine vectors sit in a per-problem slice of the
+// workspace instead (offsets index that slice) and obs / vis are read in place.
+__host__ __device__ inline LdsCarve carve_lds(int M, int N, int Pv, int kcap = 0, bool gv = false) {
   LdsCarve c;
   int off = 0;
-  c.x = off; off += Pv;
-  c.d = off; off += Pv;
-  c.g0 = off; off += Pv;
-  c.g1 = off; off += Pv;
-  c.s0 = off; off += Pv;
-  c.s1 = off; off += Pv;
-  c.hy0 = off; off += Pv;
-  c.hy1 = off; off += Pv;
-  c.hg = off; off += Pv;
-  c.obs = off; off += round_up(2 * M * N, 4);
+  int voff = 0;
+  int& o = gv ? voff : off;
+  c.x = o; o += Pv;
+  c.d = o; o += Pv;
+  c.g0 = o; o += Pv;
+  c.g1 = o; o += Pv;
+  c.s0 = o; o += Pv;
+  c.s1 = o; o += Pv;
+  c.hy0 = o; o += Pv;
+  c.hy1 = o; o += Pv;
+  c.hg = o; o += Pv;
+  c.obs = off; off += gv ? 0 : round_up(2 * M * N, 4);
   c.views = off; off += round_up(views_floats(M), 4);
   c.vpart = off; off += round_up(vpart_floats(M), 4);
   c.scratch = off; off += 2 * kWaves * 32;
@@ -66,7 +76,7 @@ __host__ __device__ inline LdsCarve carve_lds(int M, int N, int Pv, int kcap = 0
   c.hrho = off; off += round_up(kcap, 4);
   c.hc = off; off += round_up(kcap, 4);
   c.vis_bytes_off = off * 4;
-  c.total_bytes = c.vis_bytes_off + round_up(M * N, 16);
+  c.total_bytes = c.vis_bytes_off + (gv ? 0 : round_up(M * N, 16));
   return c;
 }
 
@@ -376,7 +386,7 @@ __device__ void compact_products_fused(int P, int Pv, int nh, const float* __res
   }
 }
 
-template <int MODE>
+template <int MODE, bool GV>
 __global__ __launch_bounds__(kBlock, DAVA_SOLVE_WAVES_PER_EU) void bfgs_ba_solve_kernel(SolveArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const Layout L = a.L;
@@ -384,24 +394,26 @@ __global__ __launch_bounds__(kBlock, DAVA_SOLVE_WAVES_PER_EU) void bfgs_ba_solve
   const int Pv = a.Pv;
   const int b = blockIdx.x;
   const int tid = threadIdx.x;
-  const LdsCarve cv = carve_lds(M, N, Pv, MODE == DAVA_HESSIAN_COMPACT ? a.kcap : 0);
-  float* x = lds + cv.x;
-  float* d = lds + cv.d;
-  float* g = lds + cv.g0;
-  float* gp = lds + cv.g1;
+  const LdsCarve cv = carve_lds(M, N, Pv, MODE == DAVA_HESSIAN_COMPACT ? a.kcap : 0, GV);
+  float* vb0 = GV ? a.vecs + (size_t)b * kVectors * Pv : lds;
+  float* x = vb0 + cv.x;
+  float* d = vb0 + cv.d;
+  float* g = vb0 + cv.g0;
+  float* gp = vb0 + cv.g1;
   float* hcoef = lds + cv.hcoef;
   float* hrho = lds + cv.hrho;
   float* hc = lds + cv.hc;
-  float* s_cur = lds + cv.s0;
-  float* s_pend = lds + cv.s1;
-  float* hy_new = lds + cv.hy0;
-  float* hy_pend = lds + cv.hy1;
-  float* hg = lds + cv.hg;
-  float* obs = lds + cv.obs;
+  float* s_cur = vb0 + cv.s0;
+  float* s_pend = vb0 + cv.s1;
+  float* hy_new = vb0 + cv.hy0;
+  float* hy_pend = vb0 + cv.hy1;
+  float* hg = vb0 + cv.hg;
   float* views = lds + cv.views;
   float* vpart = lds + cv.vpart;
   float* scratch = lds + cv.scratch;
-  uint8_t* vis = reinterpret_cast<uint8_t*>(lds) + cv.vis_bytes_off;
+  const int MN = M * N;
+  const float* obs = GV ? a.obs + (size_t)b * 2 * MN : lds + cv.obs;
+  const uint8_t* vis = GV ? a.vis + (size_t)b * MN : reinterpret_cast<uint8_t*>(lds) + cv.vis_bytes_off;
 
   // ---- stage the problem into LDS (zero the vector pads) ----
   const float* x0 = a.x0 + (size_t)b * P;
@@ -409,11 +421,14 @@ __global__ __launch_bounds__(kBlock, DAVA_SOLVE_WAVES_PER_EU) void bfgs_ba_solve
     x[i] = i < P ? x0[i] : 0.f;
     d[i] = g[i] = gp[i] = s_cur[i] = s_pend[i] = hy_new[i] = hy_pend[i] = hg[i] = 0.f;
   }
-  const int MN = M * N;
-  const float* ob = a.obs + (size_t)b * 2 * MN;
-  for (int i = tid; i < 2 * MN; i += kBlock) obs[i] = ob[i];
-  const uint8_t* vb = a.vis + (size_t)b * MN;
-  for (int i = tid; i < MN; i += kBlock) vis[i] = vb[i] ? 1 : 0;
+  if (!GV) {
+    float* o = lds + cv.obs;
+    uint8_t* v = reinterpret_cast<uint8_t*>(lds) + cv.vis_bytes_off;
+    const float* ob = a.obs + (size_t)b * 2 * MN;
+    for (int i = tid; i < 2 * MN; i += kBlock) o[i] = ob[i];
+    const uint8_t* vbb = a.vis + (size_t)b * MN;
+    for (int i = tid; i < MN; i += kBlock) v[i] = vbb[i] ? 1 : 0;
+  }
   __syncthreads();
 
   float* H = nullptr;   // DENSE: this problem's P x Pld inverse Hessian
@@ -622,29 +637,43 @@ struct EvalArgs {
   float* slope;
 };
 
-template <bool GRAD, bool SLOPE, bool TRIAL>
+template <bool GRAD, bool SLOPE, bool TRIAL, bool GV>
 __global__ __launch_bounds__(kBlock) void ba_evaluate_kernel(EvalArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const Layout L = a.L;
   const int P = L.P, M = L.M, N = L.N, Pv = a.Pv;
   const int b = blockIdx.x, tid = threadIdx.x;
-  const LdsCarve cv = carve_lds(M, N, Pv);
-  float* x = lds + cv.x;
-  float* d = lds + cv.d;
-  float* g = lds + cv.g0;
-  float* obs = lds + cv.obs;
+  const LdsCarve cv = carve_lds(M, N, Pv, 0, GV);
+  const int MN = M * N;
   float* views = lds + cv.views;
   float* vpart = lds + cv.vpart;
   float* scratch = lds + cv.scratch;
-  uint8_t* vis = reinterpret_cast<uint8_t*>(lds) + cv.vis_bytes_off;
-  for (int i = tid; i < Pv; i += kBlock) {
-    x[i] = i < P ? a.x[(size_t)b * P + i] : 0.f;
-    d[i] = (a.dir && i < P) ? a.dir[(size_t)b * P + i] : 0.f;
-    g[i] = 0.f;
+  const float* x;
+  const float* d;
+  float* g;
+  const float* obs;
+  const uint8_t* vis;
+  if (GV) {  // large P: work on the caller's buffers in place
+    x = a.x + (size_t)b * P;
+    d = a.dir ? a.dir + (size_t)b * P : nullptr;
+    g = a.grad ? a.grad + (size_t)b * P : nullptr;
+    obs = a.obs + (size_t)b * 2 * MN;
+    vis = a.vis + (size_t)b * MN;
+  } else {
+    float* xl = lds + cv.x;
+    float* dl = lds + cv.d;
+    float* gl = lds + cv.g0;
+    float* ol = lds + cv.obs;
+    uint8_t* vl = reinterpret_cast<uint8_t*>(lds) + cv.vis_bytes_off;
+    for (int i = tid; i < Pv; i += kBlock) {
+      xl[i] = i < P ? a.x[(size_t)b * P + i] : 0.f;
+      dl[i] = (a.dir && i < P) ? a.dir[(size_t)b * P + i] : 0.f;
+      gl[i] = 0.f;
+    }
+    for (int i = tid; i < 2 * MN; i += kBlock) ol[i] = a.obs[(size_t)b * 2 * MN + i];
+    for (int i = tid; i < MN; i += kBlock) vl[i] = a.vis[(size_t)b * MN + i] ? 1 : 0;
+    x = xl; d = dl; g = gl; obs = ol; vis = vl;
   }
-  const int MN = M * N;
-  for (int i = tid; i < 2 * MN; i += kBlock) obs[i] = a.obs[(size_t)b * 2 * MN + i];
-  for (int i = tid; i < MN; i += kBlock) vis[i] = a.vis[(size_t)b * MN + i] ? 1 : 0;
   __syncthreads();
   const float al = (TRIAL && a.alpha) ? a.alpha[b] : 0.f;
   int buf = 0;
@@ -654,7 +683,7 @@ __global__ __launch_bounds__(kBlock) void ba_evaluate_kernel(EvalArgs a) {
     a.err[b] = E;
     if (SLOPE && a.slope) a.slope[b] = sl;
   }
-  if (GRAD && a.grad)
+  if (GRAD && a.grad && !GV)
     for (int i = tid; i < P; i += kBlock) a.grad[(size_t)b * P + i] = g[i];
 }
 
@@ -672,8 +701,22 @@ static size_t dense_hessian_bytes(const DavaScene* s) {
   return (size_t)s->batch * (size_t)P * (size_t)round_up(P, 32) * sizeof(float);
 }
 
-static int lds_bytes_for(const DavaScene* s, int kcap = 0) {
-  return carve_lds(s->num_views, s->num_points, round_up(s->num_parameters, 4), kcap).total_bytes;
+#ifndef DAVA_EXTRA_LDS
+#define DAVA_EXTRA_LDS 0  // diagnostic builds only: pad LDS to force fewer workgroups per CU
+#endif
+static int lds_bytes_for(const DavaScene* s, int kcap = 0, bool gv = false) {
+  return carve_lds(s->num_views, s->num_points, round_up(s->num_parameters, 4), kcap, gv).total_bytes + DAVA_EXTRA_LDS;
+}
+
+// Global-vector mode when the all-in-LDS image would cost more than two workgroups
+// per CU (e.g. C5: P = 12381 -> 446 KB of vectors per problem).
+constexpr int kLdsModeBudget = 72 * 1024;
+static bool use_gv(const DavaScene* s, int kcap = 0) {
+  const bool force = getenv("DAVA_FORCE_GV") != nullptr;  // test knob: cross-check GV vs LDS mode
+  return force || lds_bytes_for(s, kcap, false) > kLdsModeBudget;
+}
+static size_t gv_vector_bytes(const DavaScene* s) {
+  return (size_t)s->batch * kVectors * (size_t)round_up(s->num_parameters, 4) * sizeof(float);
 }
 
 // history entries the COMPACT mode needs: one per iteration k = 1 .. iterations-1
@@ -692,9 +735,19 @@ using namespace dava;
 
 extern "C" size_t dava_ba_solve_workspace_bytes(const DavaScene* scene, const DavaSolverConfig* config) {
   if (check_scene(scene, false) != DAVA_OK || !config) return 0;
-  if (config->hessian_mode == DAVA_HESSIAN_DENSE) return dense_hessian_bytes(scene);
-  if (config->hessian_mode == DAVA_HESSIAN_COMPACT) return compact_history_bytes(scene, config);
+  const int kcap = config->hessian_mode == DAVA_HESSIAN_COMPACT ? compact_capacity(config) : 0;
+  const size_t vec = use_gv(scene, kcap) ? gv_vector_bytes(scene) : 0;
+  if (config->hessian_mode == DAVA_HESSIAN_DENSE) return vec + dense_hessian_bytes(scene);
+  if (config->hessian_mode == DAVA_HESSIAN_COMPACT) return vec + compact_history_bytes(scene, config);
   return 0;
+}
+
+template <int MODE, bool GV>
+static void launch_solve(const SolveArgs& a, int B, int lds, hipStream_t s) {
+  if (lds > 64 * 1024)
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(bfgs_ba_solve_kernel<MODE, GV>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+  hipLaunchKernelGGL((bfgs_ba_solve_kernel<MODE, GV>), dim3(B), dim3(kBlock), lds, s, a);
 }
 
 extern "C" int dava_ba_solve(const DavaScene* scene, const DavaSolverConfig* config, const float* x0,
@@ -709,10 +762,12 @@ extern "C" int dava_ba_solve(const DavaScene* scene, const DavaSolverConfig* con
   if (!x0 || !x_out) return DAVA_ERR_INVALID_ARGUMENT;
   const int kcap = mode == DAVA_HESSIAN_COMPACT ? compact_capacity(config) : 0;
   if (kcap > kMaxCompactEntries) return DAVA_ERR_UNSUPPORTED;
-  const int lds = lds_bytes_for(scene, kcap);
+  const bool gv = use_gv(scene, kcap);
+  const int lds = lds_bytes_for(scene, kcap, gv);
   if (lds > kMaxLds) return DAVA_ERR_UNSUPPORTED;
-  const size_t need = mode == DAVA_HESSIAN_DENSE ? dense_hessian_bytes(scene) : compact_history_bytes(scene, config);
-  const bool uses_ws = mode == DAVA_HESSIAN_DENSE ? config->iterations > 2 : config->iterations > 1;
+  const size_t vec = gv ? gv_vector_bytes(scene) : 0;
+  const size_t need = vec + (mode == DAVA_HESSIAN_DENSE ? dense_hessian_bytes(scene) : compact_history_bytes(scene, config));
+  const bool uses_ws = gv || (mode == DAVA_HESSIAN_DENSE ? config->iterations > 2 : config->iterations > 1);
   if (uses_ws && (!workspace || workspace_bytes < need)) return DAVA_ERR_WORKSPACE;
   SolveArgs a;
   a.L = Layout{scene->num_views, scene->num_points, scene->num_parameters, scene->distortion ? 1 : 0};
@@ -725,7 +780,8 @@ extern "C" int dava_ba_solve(const DavaScene* scene, const DavaSolverConfig* con
   a.x_out = x_out;
   a.err_out = error_out;
   a.status = status_out;
-  a.hess = static_cast<float*>(workspace);
+  a.vecs = gv ? static_cast<float*>(workspace) : nullptr;
+  a.hess = workspace ? reinterpret_cast<float*>(static_cast<char*>(workspace) + vec) : nullptr;
   a.c1 = config->sufficient_decrease;
   a.c2 = config->curvature;
   a.thr = config->error_threshold;
@@ -737,25 +793,27 @@ extern "C" int dava_ba_solve(const DavaScene* scene, const DavaSolverConfig* con
   a.kcap = kcap;
   hipStream_t s = static_cast<hipStream_t>(stream);
   if (mode == DAVA_HESSIAN_DENSE) {
-    if (lds > 64 * 1024)
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(bfgs_ba_solve_kernel<DAVA_HESSIAN_DENSE>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-    hipLaunchKernelGGL(bfgs_ba_solve_kernel<DAVA_HESSIAN_DENSE>, dim3(scene->batch), dim3(kBlock), lds, s, a);
+    if (gv) launch_solve<DAVA_HESSIAN_DENSE, true>(a, scene->batch, lds, s);
+    else launch_solve<DAVA_HESSIAN_DENSE, false>(a, scene->batch, lds, s);
   } else {
-    if (lds > 64 * 1024)
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(bfgs_ba_solve_kernel<DAVA_HESSIAN_COMPACT>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-    hipLaunchKernelGGL(bfgs_ba_solve_kernel<DAVA_HESSIAN_COMPACT>, dim3(scene->batch), dim3(kBlock), lds, s, a);
+    if (gv) launch_solve<DAVA_HESSIAN_COMPACT, true>(a, scene->batch, lds, s);
+    else launch_solve<DAVA_HESSIAN_COMPACT, false>(a, scene->batch, lds, s);
   }
   return hipGetLastError() == hipSuccess ? DAVA_OK : DAVA_ERR_LAUNCH;
 }
 
-template <bool G, bool S, bool T>
-static void launch_eval(const EvalArgs& a, int B, int lds, hipStream_t s) {
+template <bool G, bool S, bool T, bool GV>
+static void launch_eval_gv(const EvalArgs& a, int B, int lds, hipStream_t s) {
   if (lds > 64 * 1024)
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(ba_evaluate_kernel<G, S, T>),
-                        hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-  hipLaunchKernelGGL((ba_evaluate_kernel<G, S, T>), dim3(B), dim3(kBlock), lds, s, a);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(ba_evaluate_kernel<G, S, T, GV>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+  hipLaunchKernelGGL((ba_evaluate_kernel<G, S, T, GV>), dim3(B), dim3(kBlock), lds, s, a);
+}
+
+template <bool G, bool S, bool T>
+static void launch_eval(const EvalArgs& a, int B, int lds, hipStream_t s, bool gv) {
+  if (gv) launch_eval_gv<G, S, T, true>(a, B, lds, s);
+  else launch_eval_gv<G, S, T, false>(a, B, lds, s);
 }
 
 extern "C" int dava_ba_evaluate(const DavaScene* scene, const float* x, const float* direction, const float* alpha,
@@ -765,7 +823,8 @@ extern "C" int dava_ba_evaluate(const DavaScene* scene, const float* x, const fl
   if (scene->batch == 0) return DAVA_OK;
   if (!x || !error_out) return DAVA_ERR_INVALID_ARGUMENT;
   if (slope_out && !direction) return DAVA_ERR_INVALID_ARGUMENT;
-  const int lds = lds_bytes_for(scene);
+  const bool gv = use_gv(scene);
+  const int lds = lds_bytes_for(scene, 0, gv);
   if (lds > kMaxLds) return DAVA_ERR_UNSUPPORTED;
   EvalArgs a;
   a.L = Layout{scene->num_views, scene->num_points, scene->num_parameters, scene->distortion ? 1 : 0};
@@ -781,13 +840,13 @@ extern "C" int dava_ba_evaluate(const DavaScene* scene, const float* x, const fl
   hipStream_t s = static_cast<hipStream_t>(stream);
   const bool G = grad_out != nullptr, S = slope_out != nullptr, T = direction != nullptr && alpha != nullptr;
   const int B = scene->batch;
-  if (G && S && T) launch_eval<true, true, true>(a, B, lds, s);
-  else if (G && S) launch_eval<true, true, false>(a, B, lds, s);
-  else if (G && T) launch_eval<true, false, true>(a, B, lds, s);
-  else if (G) launch_eval<true, false, false>(a, B, lds, s);
-  else if (S && T) launch_eval<false, true, true>(a, B, lds, s);
-  else if (S) launch_eval<false, true, false>(a, B, lds, s);
-  else if (T) launch_eval<false, false, true>(a, B, lds, s);
-  else launch_eval<false, false, false>(a, B, lds, s);
+  if (G && S && T) launch_eval<true, true, true>(a, B, lds, s, gv);
+  else if (G && S) launch_eval<true, true, false>(a, B, lds, s, gv);
+  else if (G && T) launch_eval<true, false, true>(a, B, lds, s, gv);
+  else if (G) launch_eval<true, false, false>(a, B, lds, s, gv);
+  else if (S && T) launch_eval<false, true, true>(a, B, lds, s, gv);
+  else if (S) launch_eval<false, true, false>(a, B, lds, s, gv);
+  else if (T) launch_eval<false, false, true>(a, B, lds, s, gv);
+  else launch_eval<false, false, false>(a, B, lds, s, gv);
   return hipGetLastError() == hipSuccess ? DAVA_OK : DAVA_ERR_LAUNCH;
 }

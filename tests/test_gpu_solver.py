@@ -174,3 +174,45 @@ def test_dense_and_compact_agree_at_scale(device):
     rel = _rel(xc.cpu(), xd.cpu())
     assert (rel <= TOL).float().mean() >= 0.99, rel.max()
     assert rel.median() <= 1e-6
+
+
+def test_c5_shape_global_vector_mode_matches_oracle(device):
+    """C5 shape (16 views x 4096 points, P = 12381): the O(P) state no longer fits LDS, so the
+    kernel keeps it in HBM (GV mode) and uses the two-pass compact products.  K = 3 keeps the
+    dense-H oracle (613 MB per problem) quick."""
+    x0, obs, vis = _scene(1, 16, 4096, False, 555)
+    kw = dict(iterations=3, error_threshold=-1.0, minimum_step=-1.0)
+    ref = solver.bfgs_solve(x0, objective.ReprojectionClosure(obs, vis, 16, 4096), **kw)
+    for mode in ("compact", "dense"):
+        out, status = _gpu_solve(device, x0, obs, vis, 16, 4096, False, hessian_mode=mode, **kw)
+        assert _rel(out, ref).max() <= TOL, (mode, _rel(out, ref))
+        assert (status[:, 0] == 3).all()
+
+
+def test_c5_shape_objective_matches_oracle(device):
+    from deep_attention_visual_odometry_amd import native_ops
+
+    x, obs, vis = _scene(2, 16, 4096, False, 556)
+    d = torch.randn_like(x) * 1e-3
+    x64 = x.double().requires_grad_(True)
+    e_ref = objective.reprojection_error(x64, obs.double(), vis, 16, 4096)
+    (g_ref,) = torch.autograd.grad(e_ref.sum(), x64)
+    e, g, sl = native_ops.ba_evaluate(x.to(device), obs.to(device), vis.to(device), 16, 4096, False,
+                                      direction=d.to(device), want_grad=True, want_slope=True)
+    assert torch.allclose(e.cpu().double(), e_ref.detach(), rtol=2e-5)
+    assert ((g.cpu().double() - g_ref).norm(dim=-1) / g_ref.norm(dim=-1)).max() < 1e-4
+    sl_ref = (g_ref * d.double()).sum(-1)
+    assert torch.allclose(sl.cpu().double(), sl_ref, rtol=1e-3, atol=1e-6 * g_ref.norm().item())
+
+
+@pytest.mark.parametrize("mode", ["dense", "compact"])
+def test_global_vector_mode_equals_lds_mode(device, mode, monkeypatch):
+    """The same C3-shaped solve with the O(P) state forced into HBM (DAVA_FORCE_GV) agrees with
+    the LDS-resident kernel (same device code, different memory)."""
+    x0, obs, vis = _scene(8, 4, 256, True, 557)
+    kw = dict(iterations=30, error_threshold=-1.0, minimum_step=-1.0, hessian_mode=mode)
+    lds, _ = _gpu_solve(device, x0, obs, vis, 4, 256, True, **kw)
+    monkeypatch.setenv("DAVA_FORCE_GV", "1")
+    gv, _ = _gpu_solve(device, x0, obs, vis, 4, 256, True, **kw)
+    monkeypatch.delenv("DAVA_FORCE_GV")
+    assert _rel(gv, lds).max() <= TOL
