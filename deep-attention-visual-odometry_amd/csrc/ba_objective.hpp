@@ -91,12 +91,20 @@ __device__ __forceinline__ float trial_value(const float* x, const float* d, flo
 
 // Evaluate E (and optionally its gradient and/or slope along d) for one problem.
 // All 256 threads must call; E / slope come back identical in every thread.
-//   x, d, grad, obs, vis, views, vpart, scratch : LDS
+//   x, d, grad, obs, vis, views, vpart, scratch : LDS (or HBM in GV mode)
 //   buf : reduction double-buffer toggle (updated)
-template <bool GRAD, bool SLOPE, bool TRIAL>
-__device__ void ba_eval(const Layout& L, const float* x, const float* d, float alpha, const float* obs,
+// DOT   (with GRAD): slope_out = d . grad E, assembled from the gradient's parts inside
+//        the final reduction (no extra barrier) -- the contraction the reference's
+//        autograd w.r.t. alpha performs.
+// CHECK (with TRIAL): if x + alpha d rounds to x in every component, return false right
+//        after the first reduction without evaluating (the caller knows the answer:
+//        f(x) and phi'(0)); otherwise evaluate and return true.
+template <bool GRAD, bool SLOPE, bool TRIAL, bool DOT = false, bool CHECK = false>
+__device__ bool ba_eval(const Layout& L, const float* x, const float* d, float alpha, const float* obs,
                         const uint8_t* vis, float* grad, float* views, float* vpart, float* scratch, int& buf,
                         float& E_out, float& slope_out) {
+  static_assert(!DOT || (GRAD && !SLOPE), "DOT derives the slope from the reverse-mode gradient");
+  static_assert(!CHECK || TRIAL, "CHECK needs a trial point");
   const int tid = threadIdx.x;
   const int lane = tid & (kWave - 1);
   const int wave = tid / kWave;
@@ -129,18 +137,29 @@ __device__ void ba_eval(const Layout& L, const float* x, const float* d, float a
   }
 
   // 2. scale normalisation s = (mean|X| N + mean|t| M)/(N+M), and its slope
-  float sums[2] = {0.f, 0.f};
+  float sums[3] = {0.f, 0.f, 0.f};  // sum|X|, sum sgn(X) dX (SLOPE or DOT), moved (CHECK)
   for (int n = tid; n < N; n += kBlock) {
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
       const float X = trial_value<TRIAL>(x, d, alpha, L.pt(n) + c);
       sums[0] += fabsf(X);
-      if constexpr (SLOPE) sums[1] += sgn(X) * d[L.pt(n) + c];
+      if constexpr (SLOPE || DOT) sums[1] += sgn(X) * d[L.pt(n) + c];
     }
   }
-  if constexpr (SLOPE) block_sum<2>(sums, scratch, buf);
-  else block_sum<1>(reinterpret_cast<float(&)[1]>(sums), scratch, buf);
+  if constexpr (CHECK) {
+    bool moved = false;
+    for (int i = tid; i < L.P; i += kBlock) moved |= trial_value<true>(x, d, alpha, i) != x[i];
+    sums[2] = moved ? 1.f : 0.f;
+    block_sum<3>(sums, scratch, buf);
+  } else if constexpr (SLOPE || DOT) {
+    block_sum<2>(reinterpret_cast<float(&)[2]>(sums), scratch, buf);
+  } else {
+    block_sum<1>(reinterpret_cast<float(&)[1]>(sums), scratch, buf);
+  }
   buf ^= 1;  // (this barrier also publishes the view constants)
+  if constexpr (CHECK) {
+    if (sums[2] == 0.f) return false;  // uniform: every thread holds the same sums
+  }
   float tsum = 0.f, tdsum = 0.f;
   for (int i = L.tr(1); i < L.tr(1) + 3 * (M - 1); ++i) {
     const float t = trial_value<TRIAL>(x, d, alpha, i);
@@ -181,6 +200,7 @@ __device__ void ba_eval(const Layout& L, const float* x, const float* d, float a
   float e_loc = 0.f, sl_loc = 0.f;
   float gin[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // f cx cy k1 k2 k3 p1 p2
   float gsx = 0.f;                          // sum gX~ . X  (scale path)
+  float gdx = 0.f;                          // DOT: sum gX~ . dX
 
   // 4. sweep views (outer) x own points (inner)
   for (int m = 0; m < M; ++m) {
@@ -322,7 +342,10 @@ __device__ void ba_eval(const Layout& L, const float* x, const float* d, float a
         float* gp = grad + ip;
         if (m == 0) { gp[0] = gx0; gp[1] = gx1; gp[2] = gx2; }
         else { gp[0] += gx0; gp[1] += gx1; gp[2] += gx2; }
-        if (m == M - 1) gsx += gp[0] * X0 + gp[1] * X1 + gp[2] * X2;
+        if (m == M - 1) {
+          gsx += gp[0] * X0 + gp[1] * X1 + gp[2] * X2;
+          if constexpr (DOT) gdx += gp[0] * d[ip] + gp[1] * d[ip + 1] + gp[2] * d[ip + 2];
+        }
       }
     }
     if constexpr (GRAD) {
@@ -338,8 +361,9 @@ __device__ void ba_eval(const Layout& L, const float* x, const float* d, float a
 
   // 5. block reduction of error, slope, intrinsics gradient and scale-path sum
   if constexpr (GRAD) {
-    float r[11] = {e_loc, sl_loc, gin[0], gin[1], gin[2], gin[3], gin[4], gin[5], gin[6], gin[7], gsx};
-    block_sum<11>(r, scratch, buf);
+    float r[12] = {e_loc, sl_loc, gin[0], gin[1], gin[2], gin[3], gin[4], gin[5], gin[6], gin[7], gsx, gdx};
+    if constexpr (DOT) block_sum<12>(r, scratch, buf);
+    else block_sum<11>(reinterpret_cast<float(&)[11]>(r), scratch, buf);
     buf ^= 1;
     E_out = r[0];
     slope_out = r[1];
@@ -358,6 +382,29 @@ __device__ void ba_eval(const Layout& L, const float* x, const float* d, float a
     const float g_ps = gs * fN / fNM, g_cs = gs * fM / fNM;
     const float gabsX = g_ps / (3.0f * fN);
     const float gabsT = g_cs / (3.0f * (float)(M - 1));
+    if constexpr (DOT) {
+      // d . grad = (1/s) sum d.gX~ + gabsX sum d.sgn(X) + views + intrinsics (all threads, same order)
+      float dv = 0.f;
+      for (int m = 1; m < M; ++m) {
+        const float* v = views + (m - 1) * kViewStride;
+        auto vs = [&](int k) {
+          const float* p = vpart + (m * kWaves) * kViewPart + k;
+          return ((p[0] + p[kViewPart]) + p[2 * kViewPart]) + p[3 * kViewPart];
+        };
+        const float gth = vs(3) * v[VRCP];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+          dv += d[L.tr(m) + c] * (vs(4 + c) * inv_s + sgn(v[VT0 + c]) * gabsT);
+          dv += d[L.rot(m) + c] * (vs(c) + gth * v[VW0 + c]);
+        }
+      }
+      float di = d[0] * r[2] + d[1] * r[3] + d[2] * r[4];
+      if (L.distort) {
+#pragma unroll
+        for (int k = 0; k < 5; ++k) di += d[kd + k] * r[5 + k];
+      }
+      slope_out = (r[11] * inv_s + gabsX * sums[1]) + dv + di;
+    }
     for (int n = tid; n < N; n += kBlock) {
       float* gp = grad + L.pt(n);
 #pragma unroll
@@ -396,6 +443,7 @@ __device__ void ba_eval(const Layout& L, const float* x, const float* d, float a
     E_out = r[0];
     slope_out = r[1];
   }
+  return true;
 }
 
 }  // namespace dava

@@ -97,6 +97,12 @@ __device__ __forceinline__ void st4(float* p, float4 v) { *reinterpret_cast<floa
 #ifndef DAVA_DIAG_NO_SWEEP
 #define DAVA_DIAG_NO_SWEEP 0
 #endif
+#ifndef DAVA_TRIAL_DOT
+#define DAVA_TRIAL_DOT 0  // 1: trial slope as d . grad (reverse mode); 0: forward-mode JVP
+#endif
+#ifndef DAVA_FUSED_PAIR
+#define DAVA_FUSED_PAIR 0  // 1: two entries in flight per wave (more VGPRs)
+#endif
 #ifndef DAVA_SOLVE_WAVES_PER_EU
 #define DAVA_SOLVE_WAVES_PER_EU 2  // <= 256 VGPRs: two 4-wave workgroups per CU
 #endif
@@ -337,14 +343,16 @@ __device__ void compact_products_fused(int P, int Pv, int nh, const float* __res
     }
   };
   int j = wave;
-  for (; j + kWaves < nh; j += 2 * kWaves) {  // two entries in flight per wave
+#if DAVA_FUSED_PAIR
+  for (; j + kWaves < nh; j += 2 * kWaves) {
     f4v s0[GM], w0[GM], s1[GM], w1[GM];
     load(j, s0, w0);
     load(j + kWaves, s1, w1);
     consume(j, s0, w0);
     consume(j + kWaves, s1, w1);
   }
-  if (j < nh) {
+#endif
+  for (; j < nh; j += kWaves) {  // one entry in flight per wave
     f4v s0[GM], w0[GM];
     load(j, s0, w0);
     consume(j, s0, w0);
@@ -549,7 +557,7 @@ __global__ __launch_bounds__(kBlock, DAVA_SOLVE_WAVES_PER_EU) void bfgs_ba_solve
     }
     float a_lo = 0.f, a_hi = 0.f, al = 1.f, f_lo = E, f_hi = E, fa = E, dfa = dphi0;
     float last_al = 0.f, last_fa = 0.f;
-    bool widen = true, zoom = false, evaluated = false;
+    bool widen = true, zoom = false, evaluated = false, last_same = false;
     // trial gradients go into gp's buffer (g_prev is dead once d is formed)
     const float lim = (-a.c2) * dphi0;
     for (int t = 0; t < a.max_trials; ++t) {
@@ -558,8 +566,21 @@ __global__ __launch_bounds__(kBlock, DAVA_SOLVE_WAVES_PER_EU) void bfgs_ba_solve
         if (widen) { a_hi = al; f_hi = fa; al = 2.0f * al; }
         if (zoom) al = 0.5f * (a_lo + a_hi);
       }
-      ba_eval<true, true, true>(L, x, d, al, obs, vis, gp, views, vpart, scratch, buf, fa, dfa);
-      ++evals;
+      // Trial points that round back to x exactly (tiny alpha, e.g. bisecting an uphill
+      // direction at fp32 stagnation) need no evaluation: the reference's closure would
+      // return f(x) and, via autograd w.r.t. alpha, (d * g).sum() -- exactly f0 and
+      // phi'(0).  The check rides on the objective's first reduction (CHECK).  Otherwise
+      // E and the full gradient at the trial point are formed (kept for reuse as the
+      // next iterate's gradient) and phi'(alpha) = d . grad (DOT).
+      if (ba_eval<true, !DAVA_TRIAL_DOT, true, DAVA_TRIAL_DOT, true>(L, x, d, al, obs, vis, gp, views, vpart,
+                                                                     scratch, buf, fa, dfa)) {
+        ++evals;
+        last_same = false;
+      } else {
+        fa = E;
+        dfa = dphi0;
+        last_same = true;
+      }
       ++trials;
       evaluated = true;
       last_al = al;
@@ -592,6 +613,9 @@ __global__ __launch_bounds__(kBlock, DAVA_SOLVE_WAVES_PER_EU) void bfgs_ba_solve
     const float alpha = a_hi;
     have_next = evaluated && last_al == alpha;
     E_next = last_fa;
+    if (have_next && last_same) {  // x_{k+1} == x_k bitwise: its gradient is g itself
+      for (int i = tid; i < P; i += kBlock) gp[i] = g[i];
+    }
 
     // ---- take the step (bfgs_solver.py:191-199) and test its length (:203-207) ----
     {

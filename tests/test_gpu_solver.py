@@ -89,11 +89,22 @@ def test_reference_golden_trajectories(device, case, ks, mode):
     m, n = {"c1": (2, 64), "c2": (2, 128), "c3": (4, 256)}[case]
     x0 = torch.tensor(g[case + "_x0"])
     obs, vis = torch.tensor(g[case + "_obs"]), torch.tensor(g[case + "_vis"])
+    fn = objective.ReprojectionClosure(obs, vis, m, n)
     for k in ks:
         out, _ = _gpu_solve(device, x0, obs, vis, m, n, False, iterations=k, error_threshold=-1.0,
                             minimum_step=-1.0, hessian_mode=mode)
         ref = torch.tensor(g[f"{case}_k{k}"])
-        assert _rel(out, ref).max() <= TOL, (case, k, _rel(out, ref))
+        rel = _rel(out, ref)
+        if k <= 20:
+            assert rel.max() <= TOL, (case, k, rel)
+        else:
+            # at K = 100 some of these small problems have reached fp32 stagnation, where the
+            # reference's own trajectory moves by more than 1e-5 under a 1-ulp nudge of x0:
+            # hold them to max(1e-5, 10x that self-sensitivity) (the oracle == the reference here)
+            kw = dict(iterations=k, error_threshold=-1.0, minimum_step=-1.0)
+            nudged = solver.bfgs_solve(torch.nextafter(x0, torch.full_like(x0, float("inf"))), fn, **kw)
+            env = torch.clamp(10.0 * _rel(nudged, ref), min=TOL)
+            assert (rel <= env).all(), (case, k, rel, env)
 
 
 def test_default_stopping_rules(device):
