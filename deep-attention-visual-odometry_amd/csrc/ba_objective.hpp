@@ -100,7 +100,7 @@ __device__ __forceinline__ float trial_value(const float* x, const float* d, flo
 //        after the first reduction without evaluating (the caller knows the answer:
 //        f(x) and phi'(0)); otherwise evaluate and return true.
 template <bool GRAD, bool SLOPE, bool TRIAL, bool DOT = false, bool CHECK = false>
-__device__ bool ba_eval(const Layout& L, const float* x, const float* d, float alpha, const float* obs,
+__device__ __forceinline__ bool ba_eval(const Layout& L, const float* x, const float* d, float alpha, const float* obs,
                         const uint8_t* vis, float* grad, float* views, float* vpart, float* scratch, int& buf,
                         float& E_out, float& slope_out) {
   static_assert(!DOT || (GRAD && !SLOPE), "DOT derives the slope from the reverse-mode gradient");
@@ -138,17 +138,23 @@ __device__ bool ba_eval(const Layout& L, const float* x, const float* d, float a
 
   // 2. scale normalisation s = (mean|X| N + mean|t| M)/(N+M), and its slope
   float sums[3] = {0.f, 0.f, 0.f};  // sum|X|, sum sgn(X) dX (SLOPE or DOT), moved (CHECK)
+  bool moved = false;
   for (int n = tid; n < N; n += kBlock) {
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
       const float X = trial_value<TRIAL>(x, d, alpha, L.pt(n) + c);
       sums[0] += fabsf(X);
       if constexpr (SLOPE || DOT) sums[1] += sgn(X) * d[L.pt(n) + c];
+      if constexpr (CHECK) moved |= X != x[L.pt(n) + c];
     }
   }
   if constexpr (CHECK) {
-    bool moved = false;
-    for (int i = tid; i < L.P; i += kBlock) moved |= trial_value<true>(x, d, alpha, i) != x[i];
+    // the parameters that are not point coordinates: intrinsics, views, distortion
+    const int other = L.P - 3 * N;
+    for (int k = tid; k < other; k += kBlock) {
+      const int i = k < 3 ? k : k + 3 * N;
+      moved |= trial_value<true>(x, d, alpha, i) != x[i];
+    }
     sums[2] = moved ? 1.f : 0.f;
     block_sum<3>(sums, scratch, buf);
   } else if constexpr (SLOPE || DOT) {
@@ -286,7 +292,11 @@ __device__ bool ba_eval(const Layout& L, const float* x, const float* d, float a
         vv = vb + in.cy;
       }
       const int pair = m * N + n;
+#ifdef DAVA_WGT_CAST
+      const float wgt = (float)vis[pair];
+#else
       const float wgt = vis[pair] ? 1.0f : 0.0f;
+#endif
       const float ru = u - obs[2 * pair], rv = vv - obs[2 * pair + 1];
       e_loc += (ru * ru + rv * rv) * wgt;
       if constexpr (SLOPE) {

@@ -100,8 +100,11 @@ __device__ __forceinline__ void st4(float* p, float4 v) { *reinterpret_cast<floa
 #ifndef DAVA_TRIAL_DOT
 #define DAVA_TRIAL_DOT 0  // 1: trial slope as d . grad (reverse mode); 0: forward-mode JVP
 #endif
+#ifndef DAVA_TRIAL_CHECK
+#define DAVA_TRIAL_CHECK 1  // skip evaluating trial points that round back to x
+#endif
 #ifndef DAVA_FUSED_PAIR
-#define DAVA_FUSED_PAIR 0  // 1: two entries in flight per wave (more VGPRs)
+#define DAVA_FUSED_PAIR 1  // two history entries in flight per wave (0: one; fewer VGPRs)
 #endif
 #ifndef DAVA_SOLVE_WAVES_PER_EU
 #define DAVA_SOLVE_WAVES_PER_EU 2  // <= 256 VGPRs: two 4-wave workgroups per CU
@@ -141,7 +144,7 @@ __device__ __forceinline__ float rank2(float h, float sri, float sj, float c, fl
 // access is a contiguous row piece of up to 1 KiB.  Lane = column means the
 // column sums need no cross-lane reduction.  U rows are loaded before any is
 // consumed to keep U KiB per wave in flight.
-__device__ void dense_sweep(const Layout& L, int Pld, float* __restrict__ H, bool materialized, float gamma0,
+__device__ __forceinline__ void dense_sweep(const Layout& L, int Pld, float* __restrict__ H, bool materialized, float gamma0,
                             const float* ps, const float* phy, float prho, float pc, const float* g,
                             const float* gp, float* hy_out, float* hg_out) {
   constexpr int U = DAVA_SWEEP_ROWS;
@@ -214,7 +217,7 @@ __device__ void dense_sweep(const Layout& L, int Pld, float* __restrict__ H, boo
 // a product H v costs 2 passes over 2 nh P floats instead of a P^2 sweep.
 // Pass 1: 4 dots per entry (s.y, w.y, s.g, w.g) -> coefficients in LDS.
 // Pass 2: a = H y and b = H g as coefficient-weighted sums of the rows.
-__device__ void compact_products(int P, int Pv, int nh, const float* __restrict__ S, const float* __restrict__ W,
+__device__ __forceinline__ void compact_products(int P, int Pv, int nh, const float* __restrict__ S, const float* __restrict__ W,
                                  float* coef, const float* hrho, const float* hc, float gamma0, const float* g,
                                  const float* gp, float* a_out, float* b_out) {
   const int lane = threadIdx.x & (kWave - 1);
@@ -287,7 +290,7 @@ __device__ void compact_products(int P, int Pv, int nh, const float* __restrict_
 // added in a fixed tree ((w0 + w2) + (w1 + w3)) through 4 spare LDS vectors,
 // so the result is deterministic.  a_out / b_out / spare0..3 are Pv-float LDS vectors.
 template <int GM>
-__device__ void compact_products_fused(int P, int Pv, int nh, const float* __restrict__ S,
+__device__ __forceinline__ void compact_products_fused(int P, int Pv, int nh, const float* __restrict__ S,
                                        const float* __restrict__ W, const float* hrho, const float* hc,
                                        float gamma0, const float* g, const float* gp, float* a_out, float* b_out,
                                        float* spare0, float* spare1, float* spare2, float* spare3) {
@@ -572,7 +575,7 @@ __global__ __launch_bounds__(kBlock, DAVA_SOLVE_WAVES_PER_EU) void bfgs_ba_solve
       // phi'(0).  The check rides on the objective's first reduction (CHECK).  Otherwise
       // E and the full gradient at the trial point are formed (kept for reuse as the
       // next iterate's gradient) and phi'(alpha) = d . grad (DOT).
-      if (ba_eval<true, !DAVA_TRIAL_DOT, true, DAVA_TRIAL_DOT, true>(L, x, d, al, obs, vis, gp, views, vpart,
+      if (ba_eval<true, !DAVA_TRIAL_DOT, true, DAVA_TRIAL_DOT, DAVA_TRIAL_CHECK>(L, x, d, al, obs, vis, gp, views, vpart,
                                                                      scratch, buf, fa, dfa)) {
         ++evals;
         last_same = false;
