@@ -89,6 +89,70 @@ __device__ __forceinline__ float trial_value(const float* x, const float* d, flo
   else return x[i];
 }
 
+// ---- ray-angle residual (the error CalibrationNetwork minimises) ----------------------
+// calibration_network.py:58-67: angle between the observation's ray
+// (pixel_coordinates_to_homogeneous, geometry/homogeneous_projection.py:21-44:
+// (u - cx, v - cy, elu(f) + 1)) and the camera-relative point p, in Kahan's form
+// 2 atan2(|a^ - b^|, |a^ + b^|) with both norms clamped at 2^-52
+// (geometry/projective_plane_angle_distance.py:20-64).  Derivatives follow torch's
+// conventions: a zero norm has zero subgradient, a clamped norm passes none.
+struct RayAngle {
+  float cx, cy, F, Fp;  // principal point, focal elu(f) + 1 and its derivative
+  float dcx, dcy, dF;   // SLOPE: tangents
+};
+constexpr float kRayEps = 2.220446049250313e-16f;
+
+// unit vector x / clamp(|x|, eps) and the projection of a cotangent / tangent through it
+__device__ __forceinline__ void ray_unit_backward(float r, float n, const float (&u)[3], const float (&g)[3],
+                                                  float (&out)[3]) {
+  const float k = r >= kRayEps ? u[0] * g[0] + u[1] * g[1] + u[2] * g[2] : 0.0f;
+#pragma unroll
+  for (int c = 0; c < 3; ++c) out[c] = (g[c] - u[c] * k) / n;
+}
+
+template <bool GRAD, bool SLOPE>
+__device__ __forceinline__ void ray_angle_pair(const RayAngle& ra, const float* ob, uint8_t visible, float p0,
+                                               float p1, float p2, float dp0, float dp1, float dp2, float& e,
+                                               float& sl, float (&gin)[8], float& G0, float& G1, float& G2) {
+  const float wgt = visible ? 1.0f : 0.0f;
+  const float h[3] = {ob[0] - ra.cx, ob[1] - ra.cy, ra.F};
+  const float hr = sqrtf(h[0] * h[0] + h[1] * h[1] + h[2] * h[2]);
+  const float hn = clamp_min(hr, kRayEps);
+  const float a[3] = {h[0] / hn, h[1] / hn, h[2] / hn};
+  const float pr = sqrtf(p0 * p0 + p1 * p1 + p2 * p2);
+  const float pn = clamp_min(pr, kRayEps);
+  const float b[3] = {p0 / pn, p1 / pn, p2 / pn};
+  const float su[3] = {a[0] + b[0], a[1] + b[1], a[2] + b[2]};
+  const float df[3] = {a[0] - b[0], a[1] - b[1], a[2] - b[2]};
+  const float S = sqrtf(su[0] * su[0] + su[1] * su[1] + su[2] * su[2]);
+  const float D = sqrtf(df[0] * df[0] + df[1] * df[1] + df[2] * df[2]);
+  e += 2.0f * atan2f(D, S) * wgt;
+  const float den = S * S + D * D;
+  if constexpr (SLOPE) {
+    const float dh[3] = {-ra.dcx, -ra.dcy, ra.dF};
+    const float dp[3] = {dp0, dp1, dp2};
+    float da[3], db[3];
+    ray_unit_backward(hr, hn, a, dh, da);  // the Jacobian of x -> x/|x| is symmetric
+    ray_unit_backward(pr, pn, b, dp, db);
+    const float dS = S > 0.0f ? (su[0] * (da[0] + db[0]) + su[1] * (da[1] + db[1]) + su[2] * (da[2] + db[2])) / S : 0.0f;
+    const float dD = D > 0.0f ? (df[0] * (da[0] - db[0]) + df[1] * (da[1] - db[1]) + df[2] * (da[2] - db[2])) / D : 0.0f;
+    sl += 2.0f * wgt * (S * dD - D * dS) / den;
+  }
+  if constexpr (GRAD) {
+    const float gD = 2.0f * wgt * S / den, gS = -2.0f * wgt * D / den;  // atan2 backward
+    const float cD = D > 0.0f ? gD / D : 0.0f, cS = S > 0.0f ? gS / S : 0.0f;
+    const float ga[3] = {cS * su[0] + cD * df[0], cS * su[1] + cD * df[1], cS * su[2] + cD * df[2]};
+    const float gb[3] = {cS * su[0] - cD * df[0], cS * su[1] - cD * df[1], cS * su[2] - cD * df[2]};
+    float gh[3], gp[3];
+    ray_unit_backward(hr, hn, a, ga, gh);
+    ray_unit_backward(pr, pn, b, gb, gp);
+    gin[0] += gh[2] * ra.Fp;
+    gin[1] -= gh[0];
+    gin[2] -= gh[1];
+    G0 = gp[0]; G1 = gp[1]; G2 = gp[2];
+  }
+}
+
 // Evaluate E (and optionally its gradient and/or slope along d) for one problem.
 // All 256 threads must call; E / slope come back identical in every thread.
 //   x, d, grad, obs, vis, views, vpart, scratch : LDS (or HBM in GV mode)
@@ -99,7 +163,8 @@ __device__ __forceinline__ float trial_value(const float* x, const float* d, flo
 // CHECK (with TRIAL): if x + alpha d rounds to x in every component, return false right
 //        after the first reduction without evaluating (the caller knows the answer:
 //        f(x) and phi'(0)); otherwise evaluate and return true.
-template <bool GRAD, bool SLOPE, bool TRIAL, bool DOT = false, bool CHECK = false>
+template <bool GRAD, bool SLOPE, bool TRIAL, bool DOT = false, bool CHECK = false,
+          int RES = DAVA_RESIDUAL_SQUARED_REPROJECTION>
 __device__ __forceinline__ bool ba_eval(const Layout& L, const float* x, const float* d, float alpha, const float* obs,
                         const uint8_t* vis, float* grad, float* views, float* vpart, float* scratch, int& buf,
                         float& E_out, float& slope_out) {
@@ -203,6 +268,15 @@ __device__ __forceinline__ bool ba_eval(const Layout& L, const float* x, const f
     if (L.distort) { din.k1 = d[kd]; din.k2 = d[kd + 1]; din.k3 = d[kd + 2]; din.p1 = d[kd + 3]; din.p2 = d[kd + 4]; }
   }
 
+  RayAngle ra{};
+  if constexpr (RES == DAVA_RESIDUAL_RAY_ANGLE) {
+    ra.cx = in.cx;
+    ra.cy = in.cy;
+    ra.F = (in.f > 0.0f ? in.f : expm1f(in.f)) + 1.0f;  // elu(f) + 1
+    ra.Fp = in.f > 0.0f ? 1.0f : expf(in.f);
+    if constexpr (SLOPE) { ra.dcx = din.cx; ra.dcy = din.cy; ra.dF = ra.Fp * din.f; }
+  }
+
   float e_loc = 0.f, sl_loc = 0.f;
   float gin[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // f cx cy k1 k2 k3 p1 p2
   float gsx = 0.f;                          // sum gX~ . X  (scale path)
@@ -266,70 +340,74 @@ __device__ __forceinline__ bool ba_eval(const Layout& L, const float* x, const f
           dp2 = da2 * vc + a2 * dc + k * w2 + Avw * dw2 + e2 * vB + c2 * dB + dtt2;
         }
       }
-      // projection
-      const float iz = 1.0f / p2;
-      const float qx = p0 * iz, qy = p1 * iz;
-      const float ub = in.f * qx, vb = in.f * qy;
-      float u, vv, dub = 0.f, dvb = 0.f;
-      float Juu = 1.f, Juv = 0.f, Jvv = 1.f, r2 = 0.f;
-      if constexpr (SLOPE) {
-        const float dqx = (dp0 - qx * dp2) * iz, dqy = (dp1 - qy * dp2) * iz;
-        dub = din.f * qx + in.f * dqx;
-        dvb = din.f * qy + in.f * dqy;
-      }
-      if (L.distort) {
-        r2 = ub * ub + vb * vb;
-        const float D = 1.0f + in.k1 * r2 + in.k2 * r2 * r2 + in.k3 * r2 * r2 * r2;
-        const float Dr = in.k1 + 2.0f * in.k2 * r2 + 3.0f * in.k3 * r2 * r2;
-        const float uvb = ub * vb;
-        u = ub * D + 2.0f * in.p1 * uvb + in.p2 * (r2 + 2.0f * ub * ub) + in.cx;
-        vv = vb * D + 2.0f * in.p2 * uvb + in.p1 * (r2 + 2.0f * vb * vb) + in.cy;
-        Juu = D + 2.0f * ub * ub * Dr + 2.0f * in.p1 * vb + 6.0f * in.p2 * ub;
-        Juv = 2.0f * uvb * Dr + 2.0f * in.p1 * ub + 2.0f * in.p2 * vb;
-        Jvv = D + 2.0f * vb * vb * Dr + 2.0f * in.p2 * ub + 6.0f * in.p1 * vb;
-      } else {
-        u = ub + in.cx;
-        vv = vb + in.cy;
-      }
-      const int pair = m * N + n;
-#ifdef DAVA_WGT_CAST
-      const float wgt = (float)vis[pair];
-#else
-      const float wgt = vis[pair] ? 1.0f : 0.0f;
-#endif
-      const float ru = u - obs[2 * pair], rv = vv - obs[2 * pair + 1];
-      e_loc += (ru * ru + rv * rv) * wgt;
-      if constexpr (SLOPE) {
-        float du = Juu * dub + Juv * dvb + din.cx;
-        float dv = Juv * dub + Jvv * dvb + din.cy;
-        if (L.distort) {
-          const float r4 = r2 * r2;
-          du += ub * (r2 * din.k1 + r4 * din.k2 + r4 * r2 * din.k3) + 2.0f * ub * vb * din.p1 +
-                (r2 + 2.0f * ub * ub) * din.p2;
-          dv += vb * (r2 * din.k1 + r4 * din.k2 + r4 * r2 * din.k3) + (r2 + 2.0f * vb * vb) * din.p1 +
-                2.0f * ub * vb * din.p2;
+      float G0 = 0.f, G1 = 0.f, G2 = 0.f;  // dE/dp
+      if constexpr (RES == DAVA_RESIDUAL_SQUARED_REPROJECTION) {
+        // projection
+        const float iz = 1.0f / p2;
+        const float qx = p0 * iz, qy = p1 * iz;
+        const float ub = in.f * qx, vb = in.f * qy;
+        float u, vv, dub = 0.f, dvb = 0.f;
+        float Juu = 1.f, Juv = 0.f, Jvv = 1.f, r2 = 0.f;
+        if constexpr (SLOPE) {
+          const float dqx = (dp0 - qx * dp2) * iz, dqy = (dp1 - qy * dp2) * iz;
+          dub = din.f * qx + in.f * dqx;
+          dvb = din.f * qy + in.f * dqy;
         }
-        sl_loc += 2.0f * wgt * (ru * du + rv * dv);
+        if (L.distort) {
+          r2 = ub * ub + vb * vb;
+          const float D = 1.0f + in.k1 * r2 + in.k2 * r2 * r2 + in.k3 * r2 * r2 * r2;
+          const float Dr = in.k1 + 2.0f * in.k2 * r2 + 3.0f * in.k3 * r2 * r2;
+          const float uvb = ub * vb;
+          u = ub * D + 2.0f * in.p1 * uvb + in.p2 * (r2 + 2.0f * ub * ub) + in.cx;
+          vv = vb * D + 2.0f * in.p2 * uvb + in.p1 * (r2 + 2.0f * vb * vb) + in.cy;
+          Juu = D + 2.0f * ub * ub * Dr + 2.0f * in.p1 * vb + 6.0f * in.p2 * ub;
+          Juv = 2.0f * uvb * Dr + 2.0f * in.p1 * ub + 2.0f * in.p2 * vb;
+          Jvv = D + 2.0f * vb * vb * Dr + 2.0f * in.p2 * ub + 6.0f * in.p1 * vb;
+        } else {
+          u = ub + in.cx;
+          vv = vb + in.cy;
+        }
+        const int pair = m * N + n;
+        const float wgt = vis[pair] ? 1.0f : 0.0f;
+        const float ru = u - obs[2 * pair], rv = vv - obs[2 * pair + 1];
+        e_loc += (ru * ru + rv * rv) * wgt;
+        if constexpr (SLOPE) {
+          float du = Juu * dub + Juv * dvb + din.cx;
+          float dv = Juv * dub + Jvv * dvb + din.cy;
+          if (L.distort) {
+            const float r4 = r2 * r2;
+            du += ub * (r2 * din.k1 + r4 * din.k2 + r4 * r2 * din.k3) + 2.0f * ub * vb * din.p1 +
+                  (r2 + 2.0f * ub * ub) * din.p2;
+            dv += vb * (r2 * din.k1 + r4 * din.k2 + r4 * r2 * din.k3) + (r2 + 2.0f * vb * vb) * din.p1 +
+                  2.0f * ub * vb * din.p2;
+          }
+          sl_loc += 2.0f * wgt * (ru * du + rv * dv);
+        }
+        if constexpr (GRAD) {
+          const float gu = 2.0f * wgt * ru, gv = 2.0f * wgt * rv;
+          gin[1] += gu;
+          gin[2] += gv;
+          float gub = gu, gvb = gv;
+          if (L.distort) {
+            gub = gu * Juu + gv * Juv;
+            gvb = gu * Juv + gv * Jvv;
+            const float r4 = r2 * r2;
+            const float gr = gu * ub + gv * vb;
+            gin[3] += gr * r2;
+            gin[4] += gr * r4;
+            gin[5] += gr * r4 * r2;
+            gin[6] += gu * 2.0f * ub * vb + gv * (r2 + 2.0f * vb * vb);
+            gin[7] += gu * (r2 + 2.0f * ub * ub) + gv * 2.0f * ub * vb;
+          }
+          gin[0] += gub * qx + gvb * qy;
+          const float fi = in.f * iz;
+          G0 = gub * fi; G1 = gvb * fi; G2 = -(gub * ub + gvb * vb) * iz;
+        }
+      } else {
+        ray_angle_pair<GRAD, SLOPE>(ra, obs + 2 * (m * N + n), vis[m * N + n], p0, p1, p2, dp0, dp1, dp2,
+                                    e_loc, sl_loc, gin, G0, G1, G2);
       }
       if constexpr (GRAD) {
-        const float gu = 2.0f * wgt * ru, gv = 2.0f * wgt * rv;
-        gin[1] += gu;
-        gin[2] += gv;
-        float gub = gu, gvb = gv;
-        if (L.distort) {
-          gub = gu * Juu + gv * Juv;
-          gvb = gu * Juv + gv * Jvv;
-          const float r4 = r2 * r2;
-          const float gr = gu * ub + gv * vb;
-          gin[3] += gr * r2;
-          gin[4] += gr * r4;
-          gin[5] += gr * r4 * r2;
-          gin[6] += gu * 2.0f * ub * vb + gv * (r2 + 2.0f * vb * vb);
-          gin[7] += gu * (r2 + 2.0f * ub * ub) + gv * 2.0f * ub * vb;
-        }
-        gin[0] += gub * qx + gvb * qy;
-        const float fi = in.f * iz;
-        const float G0 = gub * fi, G1 = gvb * fi, G2 = -(gub * ub + gvb * vb) * iz;
         float gx0, gx1, gx2;
         if (m == 0) {
           gx0 = G0; gx1 = G1; gx2 = G2;

@@ -397,7 +397,7 @@ __device__ __forceinline__ void compact_products_fused(int P, int Pv, int nh, co
   }
 }
 
-template <int MODE, bool GV>
+template <int MODE, bool GV, int RES>
 __global__ __launch_bounds__(kBlock, DAVA_SOLVE_WAVES_PER_EU) void bfgs_ba_solve_kernel(SolveArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const Layout L = a.L;
@@ -467,7 +467,8 @@ __global__ __launch_bounds__(kBlock, DAVA_SOLVE_WAVES_PER_EU) void bfgs_ba_solve
     if (have_next) {
       E = E_next;
     } else {
-      ba_eval<true, false, false>(L, x, nullptr, 0.f, obs, vis, g, views, vpart, scratch, buf, E, unused);
+      ba_eval<true, false, false, false, false, RES>(L, x, nullptr, 0.f, obs, vis, g, views, vpart, scratch, buf, E,
+                                                     unused);
       ++evals;
     }
     if (!(E > a.thr)) { reason = DAVA_STOP_ERROR; break; }
@@ -575,7 +576,7 @@ __global__ __launch_bounds__(kBlock, DAVA_SOLVE_WAVES_PER_EU) void bfgs_ba_solve
       // phi'(0).  The check rides on the objective's first reduction (CHECK).  Otherwise
       // E and the full gradient at the trial point are formed (kept for reuse as the
       // next iterate's gradient) and phi'(alpha) = d . grad (DOT).
-      if (ba_eval<true, !DAVA_TRIAL_DOT, true, DAVA_TRIAL_DOT, DAVA_TRIAL_CHECK>(L, x, d, al, obs, vis, gp, views, vpart,
+      if (ba_eval<true, !DAVA_TRIAL_DOT, true, DAVA_TRIAL_DOT, DAVA_TRIAL_CHECK, RES>(L, x, d, al, obs, vis, gp, views, vpart,
                                                                      scratch, buf, fa, dfa)) {
         ++evals;
         last_same = false;
@@ -641,7 +642,8 @@ __global__ __launch_bounds__(kBlock, DAVA_SOLVE_WAVES_PER_EU) void bfgs_ba_solve
   for (int i = tid; i < P; i += kBlock) xo[i] = x[i];
   if (a.err_out) {
     float e2 = 0.f;
-    ba_eval<false, false, false>(L, x, nullptr, 0.f, obs, vis, nullptr, views, vpart, scratch, buf, e2, unused);
+    ba_eval<false, false, false, false, false, RES>(L, x, nullptr, 0.f, obs, vis, nullptr, views, vpart, scratch, buf,
+                                                   e2, unused);
     if (tid == 0) a.err_out[b] = e2;
   }
   if (a.status && tid == 0) {
@@ -664,7 +666,7 @@ struct EvalArgs {
   float* slope;
 };
 
-template <bool GRAD, bool SLOPE, bool TRIAL, bool GV>
+template <bool GRAD, bool SLOPE, bool TRIAL, bool GV, int RES>
 __global__ __launch_bounds__(kBlock) void ba_evaluate_kernel(EvalArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const Layout L = a.L;
@@ -705,7 +707,7 @@ __global__ __launch_bounds__(kBlock) void ba_evaluate_kernel(EvalArgs a) {
   const float al = (TRIAL && a.alpha) ? a.alpha[b] : 0.f;
   int buf = 0;
   float E = 0.f, sl = 0.f;
-  ba_eval<GRAD, SLOPE, TRIAL>(L, x, d, al, obs, vis, g, views, vpart, scratch, buf, E, sl);
+  ba_eval<GRAD, SLOPE, TRIAL, false, false, RES>(L, x, d, al, obs, vis, g, views, vpart, scratch, buf, E, sl);
   if (tid == 0) {
     a.err[b] = E;
     if (SLOPE && a.slope) a.slope[b] = sl;
@@ -720,6 +722,9 @@ static int check_scene(const DavaScene* s, bool need_data = true) {
   const int P = 3 + 3 * s->num_points + 6 * (s->num_views - 1) + (s->distortion ? 5 : 0);
   if (s->num_parameters != P) return DAVA_ERR_INVALID_ARGUMENT;
   if (need_data && s->batch > 0 && (!s->observations || !s->visibility)) return DAVA_ERR_INVALID_ARGUMENT;
+  if (s->residual != DAVA_RESIDUAL_SQUARED_REPROJECTION && s->residual != DAVA_RESIDUAL_RAY_ANGLE)
+    return DAVA_ERR_INVALID_ARGUMENT;
+  if (s->residual == DAVA_RESIDUAL_RAY_ANGLE && s->distortion) return DAVA_ERR_UNSUPPORTED;
   return DAVA_OK;
 }
 
@@ -769,12 +774,18 @@ extern "C" size_t dava_ba_solve_workspace_bytes(const DavaScene* scene, const Da
   return 0;
 }
 
-template <int MODE, bool GV>
-static void launch_solve(const SolveArgs& a, int B, int lds, hipStream_t s) {
+template <int MODE, bool GV, int RES>
+static void launch_solve_res(const SolveArgs& a, int B, int lds, hipStream_t s) {
   if (lds > 64 * 1024)
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(bfgs_ba_solve_kernel<MODE, GV>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(bfgs_ba_solve_kernel<MODE, GV, RES>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-  hipLaunchKernelGGL((bfgs_ba_solve_kernel<MODE, GV>), dim3(B), dim3(kBlock), lds, s, a);
+  hipLaunchKernelGGL((bfgs_ba_solve_kernel<MODE, GV, RES>), dim3(B), dim3(kBlock), lds, s, a);
+}
+
+template <int MODE, bool GV>
+static void launch_solve(const SolveArgs& a, int B, int lds, hipStream_t s, int residual) {
+  if (residual == DAVA_RESIDUAL_RAY_ANGLE) launch_solve_res<MODE, GV, DAVA_RESIDUAL_RAY_ANGLE>(a, B, lds, s);
+  else launch_solve_res<MODE, GV, DAVA_RESIDUAL_SQUARED_REPROJECTION>(a, B, lds, s);
 }
 
 extern "C" int dava_ba_solve(const DavaScene* scene, const DavaSolverConfig* config, const float* x0,
@@ -820,27 +831,33 @@ extern "C" int dava_ba_solve(const DavaScene* scene, const DavaSolverConfig* con
   a.kcap = kcap;
   hipStream_t s = static_cast<hipStream_t>(stream);
   if (mode == DAVA_HESSIAN_DENSE) {
-    if (gv) launch_solve<DAVA_HESSIAN_DENSE, true>(a, scene->batch, lds, s);
-    else launch_solve<DAVA_HESSIAN_DENSE, false>(a, scene->batch, lds, s);
+    if (gv) launch_solve<DAVA_HESSIAN_DENSE, true>(a, scene->batch, lds, s, scene->residual);
+    else launch_solve<DAVA_HESSIAN_DENSE, false>(a, scene->batch, lds, s, scene->residual);
   } else {
-    if (gv) launch_solve<DAVA_HESSIAN_COMPACT, true>(a, scene->batch, lds, s);
-    else launch_solve<DAVA_HESSIAN_COMPACT, false>(a, scene->batch, lds, s);
+    if (gv) launch_solve<DAVA_HESSIAN_COMPACT, true>(a, scene->batch, lds, s, scene->residual);
+    else launch_solve<DAVA_HESSIAN_COMPACT, false>(a, scene->batch, lds, s, scene->residual);
   }
   return hipGetLastError() == hipSuccess ? DAVA_OK : DAVA_ERR_LAUNCH;
 }
 
-template <bool G, bool S, bool T, bool GV>
+template <bool G, bool S, bool T, bool GV, int RES>
 static void launch_eval_gv(const EvalArgs& a, int B, int lds, hipStream_t s) {
   if (lds > 64 * 1024)
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(ba_evaluate_kernel<G, S, T, GV>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(ba_evaluate_kernel<G, S, T, GV, RES>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-  hipLaunchKernelGGL((ba_evaluate_kernel<G, S, T, GV>), dim3(B), dim3(kBlock), lds, s, a);
+  hipLaunchKernelGGL((ba_evaluate_kernel<G, S, T, GV, RES>), dim3(B), dim3(kBlock), lds, s, a);
 }
 
 template <bool G, bool S, bool T>
-static void launch_eval(const EvalArgs& a, int B, int lds, hipStream_t s, bool gv) {
-  if (gv) launch_eval_gv<G, S, T, true>(a, B, lds, s);
-  else launch_eval_gv<G, S, T, false>(a, B, lds, s);
+static void launch_eval(const EvalArgs& a, int B, int lds, hipStream_t s, bool gv, int res) {
+  constexpr int SQ = DAVA_RESIDUAL_SQUARED_REPROJECTION, RAY = DAVA_RESIDUAL_RAY_ANGLE;
+  if (res == RAY) {
+    if (gv) launch_eval_gv<G, S, T, true, RAY>(a, B, lds, s);
+    else launch_eval_gv<G, S, T, false, RAY>(a, B, lds, s);
+  } else {
+    if (gv) launch_eval_gv<G, S, T, true, SQ>(a, B, lds, s);
+    else launch_eval_gv<G, S, T, false, SQ>(a, B, lds, s);
+  }
 }
 
 extern "C" int dava_ba_evaluate(const DavaScene* scene, const float* x, const float* direction, const float* alpha,
@@ -867,13 +884,13 @@ extern "C" int dava_ba_evaluate(const DavaScene* scene, const float* x, const fl
   hipStream_t s = static_cast<hipStream_t>(stream);
   const bool G = grad_out != nullptr, S = slope_out != nullptr, T = direction != nullptr && alpha != nullptr;
   const int B = scene->batch;
-  if (G && S && T) launch_eval<true, true, true>(a, B, lds, s, gv);
-  else if (G && S) launch_eval<true, true, false>(a, B, lds, s, gv);
-  else if (G && T) launch_eval<true, false, true>(a, B, lds, s, gv);
-  else if (G) launch_eval<true, false, false>(a, B, lds, s, gv);
-  else if (S && T) launch_eval<false, true, true>(a, B, lds, s, gv);
-  else if (S) launch_eval<false, true, false>(a, B, lds, s, gv);
-  else if (T) launch_eval<false, false, true>(a, B, lds, s, gv);
-  else launch_eval<false, false, false>(a, B, lds, s, gv);
+  if (G && S && T) launch_eval<true, true, true>(a, B, lds, s, gv, scene->residual);
+  else if (G && S) launch_eval<true, true, false>(a, B, lds, s, gv, scene->residual);
+  else if (G && T) launch_eval<true, false, true>(a, B, lds, s, gv, scene->residual);
+  else if (G) launch_eval<true, false, false>(a, B, lds, s, gv, scene->residual);
+  else if (S && T) launch_eval<false, true, true>(a, B, lds, s, gv, scene->residual);
+  else if (S) launch_eval<false, true, false>(a, B, lds, s, gv, scene->residual);
+  else if (T) launch_eval<false, false, true>(a, B, lds, s, gv, scene->residual);
+  else launch_eval<false, false, false>(a, B, lds, s, gv, scene->residual);
   return hipGetLastError() == hipSuccess ? DAVA_OK : DAVA_ERR_LAUNCH;
 }

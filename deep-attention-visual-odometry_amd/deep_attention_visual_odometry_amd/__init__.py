@@ -6,12 +6,13 @@ Drop-in for the hot path of jskinn/deep-attention-visual-odometry
 ``_lib/libdava_ba.so`` (C ABI: include/dava_ba.h); there is no CPU path.
 """
 from .autograd_solvers import BFGSSolver, line_search_wolfe_conditions
-from .camera_model import ReprojectionError, num_parameters, unpack_calibration_parameters
+from .camera_model import RayAngleError, ReprojectionError, num_parameters, unpack_calibration_parameters
 from .scenes import make_scenes
 
 __all__ = [
     "BFGSSolver",
     "line_search_wolfe_conditions",
+    "RayAngleError",
     "ReprojectionError",
     "num_parameters",
     "unpack_calibration_parameters",

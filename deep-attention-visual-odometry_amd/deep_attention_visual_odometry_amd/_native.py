@@ -18,6 +18,9 @@ LIB_PATH = os.environ.get("DAVA_LIB") or os.path.join(_HERE, "_lib", "libdava_ba
 DAVA_OK = 0
 DAVA_HESSIAN_DENSE = 0
 DAVA_HESSIAN_COMPACT = 1
+DAVA_RESIDUAL_SQUARED_REPROJECTION = 0
+DAVA_RESIDUAL_RAY_ANGLE = 1
+ABI_VERSION = 2  # include/dava_ba.h DAVA_ABI_VERSION
 STOP_ITERATIONS, STOP_ERROR, STOP_STEP = 0, 1, 2
 STATUS_WORDS = 4
 
@@ -35,6 +38,7 @@ class DavaScene(ctypes.Structure):
         ("num_parameters", _c_i32),
         ("observations", _vp),
         ("visibility", _vp),
+        ("residual", _c_i32),
     ]
 
 
@@ -96,7 +100,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args
-        if lib.dava_abi_version() != 1:
+        if lib.dava_abi_version() != ABI_VERSION:
             raise NativeLibraryError("libdava_ba.so ABI version mismatch")
         _lib = lib
         return lib

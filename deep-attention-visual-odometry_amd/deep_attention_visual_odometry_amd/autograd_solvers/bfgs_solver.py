@@ -102,7 +102,7 @@ class BFGSSolver(Module):
             fn.visibility.reshape(-1, fn.num_views, fn.num_points), fn.num_views, fn.num_points, fn.distortion,
             sufficient_decrease=self.sufficient_decrease, curvature=self.curvature,
             error_threshold=error_threshold, iterations=num_iterations, minimum_step=self.minimum_step,
-            hessian_mode=mode, want_status=True)
+            hessian_mode=mode, want_status=True, residual=fn.residual)
         self.last_status = status
         return x.reshape(parameters.shape)
 

@@ -49,9 +49,9 @@ class _NativeObjective(torch.autograd.Function):
     """E(x) per row with dE/dx from the HIP reverse-mode kernel (first order only)."""
 
     @staticmethod
-    def forward(ctx, x, observations, visibility, num_views, num_points, distortion):
+    def forward(ctx, x, observations, visibility, num_views, num_points, distortion, residual):
         err, grad, _ = native_ops.ba_evaluate(x, observations, visibility, num_views, num_points, distortion,
-                                              want_grad=ctx.needs_input_grad[0])
+                                              want_grad=ctx.needs_input_grad[0], residual=residual)
         ctx.save_for_backward(grad if grad is not None else err)
         return err
 
@@ -59,7 +59,7 @@ class _NativeObjective(torch.autograd.Function):
     @torch.autograd.function.once_differentiable
     def backward(ctx, grad_out):
         (grad,) = ctx.saved_tensors
-        return grad_out.unsqueeze(-1) * grad, None, None, None, None, None
+        return grad_out.unsqueeze(-1) * grad, None, None, None, None, None, None
 
 
 class ReprojectionError:
@@ -87,6 +87,8 @@ class ReprojectionError:
         self.num_points = int(num_points)
         self.distortion = bool(distortion)
 
+    residual = native_ops.N.DAVA_RESIDUAL_SQUARED_REPROJECTION
+
     @property
     def num_parameters(self) -> int:
         return num_parameters(self.num_views, self.num_points, self.distortion)
@@ -106,5 +108,24 @@ class ReprojectionError:
         vis = vis.reshape(-1, self.num_views, self.num_points)
         if x.dtype != torch.float32:
             raise TypeError("ReprojectionError evaluates in float32")
-        err = _NativeObjective.apply(x, obs, vis, self.num_views, self.num_points, self.distortion)
+        err = _NativeObjective.apply(x, obs, vis, self.num_views, self.num_points, self.distortion, self.residual)
         return err.reshape(lead)
+
+
+class RayAngleError(ReprojectionError):
+    """The error ``CalibrationNetwork`` minimises (``networks/calibration_network.py:58-67``):
+
+    E(x) = sum_{m,n} vis[m,n] * angle(ray(obs[m,n]), p_m(X_n))
+
+    with ray(u, v) = (u - cx, v - cy, elu(f) + 1)
+    (``geometry/homogeneous_projection.py:21-44``), p_m(X_n) the scale-normalised
+    camera-relative point (``camera_model/calibration_pinhole_camera_model.py:78-117``)
+    and the angle in Kahan's form 2 atan2(|a^ - b^|, |a^ + b^|)
+    (``geometry/projective_plane_angle_distance.py:20-64``).  Pinhole parameter
+    layout only; the fused solver and the evaluation kernel both run it on the GPU.
+    """
+
+    residual = native_ops.N.DAVA_RESIDUAL_RAY_ANGLE
+
+    def __init__(self, observations: torch.Tensor, visibility: torch.Tensor, num_views: int, num_points: int):
+        super().__init__(observations, visibility, num_views, num_points, distortion=False)

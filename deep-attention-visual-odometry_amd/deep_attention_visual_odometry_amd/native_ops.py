@@ -23,15 +23,16 @@ def _c(t: torch.Tensor) -> torch.Tensor:
 
 
 def scene_struct(observations: torch.Tensor, visibility: torch.Tensor, num_views: int, num_points: int,
-                 distortion: bool, batch: int) -> N.DavaScene:
+                 distortion: bool, batch: int, residual: int = N.DAVA_RESIDUAL_SQUARED_REPROJECTION) -> N.DavaScene:
     p = 3 + 3 * num_points + 6 * (num_views - 1) + (5 if distortion else 0)
     return N.DavaScene(batch, num_views, num_points, 1 if distortion else 0, p,
-                       N.ptr(observations), N.ptr(visibility))
+                       N.ptr(observations), N.ptr(visibility), residual)
 
 
 def ba_evaluate(x: torch.Tensor, observations: torch.Tensor, visibility: torch.Tensor, num_views: int,
                 num_points: int, distortion: bool = False, direction: Optional[torch.Tensor] = None,
-                alpha: Optional[torch.Tensor] = None, want_grad: bool = True, want_slope: bool = False
+                alpha: Optional[torch.Tensor] = None, want_grad: bool = True, want_slope: bool = False,
+                residual: int = N.DAVA_RESIDUAL_SQUARED_REPROJECTION,
                 ) -> Tuple[torch.Tensor, Optional[torch.Tensor], Optional[torch.Tensor]]:
     """E, dE/dx, d.dE/dx at x + alpha*direction for a (B, P) fp32 batch."""
     lib = N.load_library()
@@ -47,7 +48,7 @@ def ba_evaluate(x: torch.Tensor, observations: torch.Tensor, visibility: torch.T
     err = torch.empty(b, device=x.device, dtype=torch.float32)
     grad = torch.empty_like(x) if want_grad else None
     slope = torch.empty(b, device=x.device, dtype=torch.float32) if want_slope else None
-    sc = scene_struct(obs, vis, num_views, num_points, distortion, b)
+    sc = scene_struct(obs, vis, num_views, num_points, distortion, b, residual)
     with torch.cuda.device(x.device):
         N.check(lib.dava_ba_evaluate(sc, N.ptr(x), N.ptr(d), N.ptr(a), N.ptr(err), N.ptr(grad), N.ptr(slope),
                                      N.stream_of(x.device)), "dava_ba_evaluate")
@@ -58,7 +59,8 @@ def ba_solve(x0: torch.Tensor, observations: torch.Tensor, visibility: torch.Ten
              num_points: int, distortion: bool, *, sufficient_decrease: float = 1e-4, curvature: float = 0.9,
              error_threshold: float = 1e-4, iterations: int = 1000, minimum_step: float = 1e-8,
              max_line_search_trials: int = 1000, strong: bool = True, hessian_mode: int = N.DAVA_HESSIAN_DENSE,
-             want_error: bool = False, want_status: bool = False, workspace: Optional[torch.Tensor] = None):
+             want_error: bool = False, want_status: bool = False, workspace: Optional[torch.Tensor] = None,
+             residual: int = N.DAVA_RESIDUAL_SQUARED_REPROJECTION):
     """One fused launch for the whole batch.  Returns (x, error|None, status|None)."""
     lib = N.load_library()
     N.require_device_tensor(x0, "parameters")
@@ -69,7 +71,7 @@ def ba_solve(x0: torch.Tensor, observations: torch.Tensor, visibility: torch.Ten
     dev = x0.device
     obs = _c(observations.detach().to(device=dev, dtype=torch.float32))
     vis = _c(visibility.detach().to(device=dev, dtype=torch.uint8))
-    sc = scene_struct(obs, vis, num_views, num_points, distortion, b)
+    sc = scene_struct(obs, vis, num_views, num_points, distortion, b, residual)
     cfg = N.DavaSolverConfig(float(sufficient_decrease), float(curvature), float(error_threshold),
                              float(minimum_step), int(iterations), int(max_line_search_trials),
                              1 if strong else 0, int(hessian_mode))

@@ -114,8 +114,18 @@ def make_scenes(
     first_index: int = 0,
     initial_noise: float = 0.01,
     drop: float = 0.0,
+    ray_angle: bool = False,
 ) -> SceneBatch:
-    """Problems ``first_index .. first_index + batch - 1`` of the stream ``seed``."""
+    """Problems ``first_index .. first_index + batch - 1`` of the stream ``seed``.
+
+    ``ray_angle=True`` stores the focal slot in the parameterisation of the ray-angle
+    objective (focal = elu(x[0]) + 1, ``geometry/homogeneous_projection.py:21-44``), so
+    the truth is an exact zero of ``RayAngleError``; the observations are unchanged.
+    """
+    if num_views < 2:
+        raise ValueError("num_views must be >= 2 (the scale normalisation needs a translation)")
+    if ray_angle and distortion:
+        raise ValueError("the ray-angle objective is pinhole only")
     if num_views < 2:
         raise ValueError("num_views must be >= 2 (the scale normalisation needs a translation)")
     p = parameter_count(num_views, num_points, distortion)
@@ -150,8 +160,10 @@ def make_scenes(
         else:
             raise RuntimeError("could not place points inside every view")
         x = _pack(f, c, pts[:num_points], t, w, k)
-        truth[b] = x
         obs[b] = project_truth(x, num_views, num_points, distortion)
+        if ray_angle:  # elu(x0) + 1 == f
+            x[0] = f - 1.0 if f > 1.0 else np.log(f)
+        truth[b] = x
         vis[b] = True if drop <= 0.0 else rng.random((num_views, num_points)) >= drop
         kick = initial_noise * rng.standard_normal(p)
         if distortion:

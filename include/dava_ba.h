@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define DAVA_ABI_VERSION 1
+#define DAVA_ABI_VERSION 2
 
 enum DavaStatus {
   DAVA_OK = 0,
@@ -58,6 +58,17 @@ enum DavaStopReason {
   DAVA_STOP_STEP = 2        /* ||step|| <= minimum_step (or NaN)      */
 };
 
+/* Per-(view, point) residual summed into the objective.
+ *  SQUARED_REPROJECTION: vis * |pi(X) - obs|^2  -- the benchmark objective.
+ *  RAY_ANGLE: vis * angle(ray(obs), p) with ray(obs) = (u - cx, v - cy, elu(f) + 1) and p the
+ *    camera-relative point: the error CalibrationNetwork minimises (calibration_network.py:58-67,
+ *    geometry/homogeneous_projection.py:21-44, geometry/projective_plane_angle_distance.py:20-64).
+ *    Pinhole only (distortion must be 0).                                                      */
+enum DavaResidual {
+  DAVA_RESIDUAL_SQUARED_REPROJECTION = 0,
+  DAVA_RESIDUAL_RAY_ANGLE = 1
+};
+
 /* A batch of independent calibration problems.
  * Parameter layout per problem (calibration_pinhole_camera_model.py:33-75):
  *   [f, cx, cy | X_0..X_{N-1} (xyz) | t_1..t_{M-1} | w_1..w_{M-1} | k1 k2 k3 p1 p2 (if distortion)]
@@ -70,6 +81,7 @@ typedef struct DavaScene {
   int32_t num_parameters;      /* P                                    */
   const float* observations;   /* (B, M, N, 2) fp32                    */
   const uint8_t* visibility;   /* (B, M, N) 0/1                        */
+  int32_t residual;            /* DavaResidual                         */
 } DavaScene;
 
 /* Mirrors the eval-mode BFGSSolver constructor (bfgs_solver.py:49-78). */
@@ -93,8 +105,8 @@ size_t dava_ba_solve_workspace_bytes(const DavaScene* scene, const DavaSolverCon
 
 /* The whole eval-mode solve, one launch.
  * Replaces BFGSSolver.forward(parameters, error_function)
- * (autograd_solvers/bfgs_solver.py:80-215) with error_function = the squared
- * reprojection objective over `scene`, including line_search_wolfe_conditions
+ * (autograd_solvers/bfgs_solver.py:80-215) with error_function = the objective
+ * over `scene` (its `residual`), including line_search_wolfe_conditions
  * (autograd_solvers/line_search/wolfe_conditions.py:23-239, strong=True).
  *   x0        (B, P) fp32 initial guess
  *   x_out     (B, P) fp32 result (may alias x0)

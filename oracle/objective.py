@@ -138,3 +138,54 @@ class ReprojectionClosure:
         return reprojection_error(
             x, self.observations[mask], self.visibility[mask], self.num_views, self.num_points, self.distortion
         )
+
+
+# ---- ray-angle residual (the error CalibrationNetwork minimises) ----------------------
+
+def homogeneous_rays(observations: torch.Tensor, intrinsics: torch.Tensor) -> torch.Tensor:
+    """(u - cx, v - cy, elu(f) + 1): ``geometry/homogeneous_projection.py:21-44``."""
+    focal = torch.nn.functional.elu(intrinsics[..., 0:1]) + 1.0
+    centred = observations - intrinsics[..., 1:3]
+    return torch.cat([centred, focal.expand(centred.shape[:-1] + (-1,))], dim=-1)
+
+
+def projective_plane_angle_distance(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    """2 atan2(|a^ - b^|, |a^ + b^|), norms clamped at 2^-52
+    (``geometry/projective_plane_angle_distance.py:20-64``)."""
+    a = a / torch.linalg.vector_norm(a, dim=-1, keepdim=True).clamp(min=2.220446049250313e-16)
+    b = b / torch.linalg.vector_norm(b, dim=-1, keepdim=True).clamp(min=2.220446049250313e-16)
+    total = torch.linalg.vector_norm(a + b, dim=-1)
+    diff = torch.linalg.vector_norm(a - b, dim=-1)
+    return 2.0 * torch.atan2(diff, total)
+
+
+def ray_angle_error(
+    x: torch.Tensor,
+    observations: torch.Tensor,
+    visibility: torch.Tensor,
+    num_views: int,
+    num_points: int,
+) -> torch.Tensor:
+    """``CalibrationNetwork.forward``'s error_function (``networks/calibration_network.py:58-67``):
+    sum_{m,n} vis * angle(ray(obs), p), p from the keepdim restatement of
+    ``get_camera_relative_points``."""
+    parts = split_parameters(x, num_views, num_points, False)
+    rays = homogeneous_rays(observations, parts.intrinsics)
+    p = view_points(parts.points, parts.translations, parts.rotations)
+    distance = projective_plane_angle_distance(rays, p)
+    return (distance * visibility).sum(dim=(-1, -2))
+
+
+class RayAngleClosure:
+    """``error_function(parameters, batch_mask)`` over the ray-angle objective."""
+
+    def __init__(self, observations, visibility, num_views, num_points):
+        self.observations = observations
+        self.visibility = visibility
+        self.num_views = num_views
+        self.num_points = num_points
+        self.calls = 0
+
+    def __call__(self, x: torch.Tensor, mask: torch.Tensor) -> torch.Tensor:
+        self.calls += 1
+        return ray_angle_error(x, self.observations[mask], self.visibility[mask], self.num_views, self.num_points)

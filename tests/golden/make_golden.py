@@ -24,6 +24,13 @@ Fixtures written:
                           ``scale_initial_inverse_hessian`` on random inputs.
 * ``line_search.npz`` -- ``line_search_wolfe_conditions`` alphas (strong and
                           weak) on BA objectives along the negative gradient.
+* ``ray_angle.npz``   -- the ray-angle error of ``CalibrationNetwork.forward``'s
+                          error_function (calibration_network.py:58-67, composed
+                          from the reference's own pixel_coordinates_to_homogeneous,
+                          get_camera_relative_points and projective_plane_angle_distance)
+                          with its autograd gradient (fp64, fp32; C1/C2/C3 shapes at
+                          B = 1), and BFGSSolver(...).eval() results on it after K in
+                          {5, 20} (C1, C2 shapes) and K = 100 (C1).
 * ``bfgs_traj.npz``   -- ``BFGSSolver(...).eval()`` results after K in
                           {5, 20, 100} iterations (error_threshold = -1,
                           minimum_step = -1) for C1 (2x64), C2 (2x128) and
@@ -55,7 +62,9 @@ from deep_attention_visual_odometry.camera_model import (  # noqa: E402
     unpack_calibration_parameters,
 )
 from deep_attention_visual_odometry.geometry import (  # noqa: E402
+    pixel_coordinates_to_homogeneous,
     project_points_basic_pinhole,
+    projective_plane_angle_distance,
     rotate_vector_axis_angle,
 )
 
@@ -202,9 +211,55 @@ def gen_trajectories():
     np.savez_compressed(os.path.join(HERE, "bfgs_traj.npz"), **out)
 
 
+def ref_ray_angle(x, obs, vis, m, n):
+    """calibration_network.py:58-67 verbatim in composition (B > 1 uses the keepdim scale)."""
+    parts = unpack_calibration_parameters(x, m, n)
+    rays = pixel_coordinates_to_homogeneous(obs, parts.intrinsics)
+    rel = ref_relative_points(parts.world_points, parts.camera_translations, parts.camera_rotations, x.shape[0])
+    distance = projective_plane_angle_distance(rays, rel)
+    return (distance * vis).sum(dim=(-1, -2))
+
+
+def gen_ray_angle():
+    out = {}
+    for name, (m, n) in SHAPES.items():
+        for dt_name, dt in (("f64", torch.float64), ("f32", torch.float32)):
+            s = make_scenes(1, m, n, seed=7401, drop=0.1, ray_angle=True)
+            x0 = torch.tensor(s.initial, dtype=dt)
+            obs = torch.tensor(s.observations, dtype=dt)
+            vis = torch.tensor(s.visibility)
+            x = x0.clone().requires_grad_(True)
+            e = ref_ray_angle(x, obs, vis, m, n)
+            (g,) = torch.autograd.grad(e.sum(), x)
+            key = f"eval_{name}_{dt_name}"
+            out[key + "_x"] = x0.numpy()
+            out[key + "_obs"] = obs.numpy()
+            out[key + "_vis"] = vis.numpy()
+            out[key + "_err"] = e.detach().numpy()
+            out[key + "_grad"] = g.numpy()
+    for name, batch, ks in (("c1", 4, (5, 20, 100)), ("c2", 2, (5, 20))):
+        m, n = SHAPES[name]
+        s = make_scenes(batch, m, n, seed=7402, drop=0.1, ray_angle=True)
+        x0 = torch.tensor(s.initial)
+        obs = torch.tensor(s.observations)
+        vis = torch.tensor(s.visibility)
+
+        def fn(x, mask, obs=obs, vis=vis, m=m, n=n):
+            return ref_ray_angle(x, obs[mask], vis[mask], m, n)
+
+        key = f"traj_{name}"
+        out[key + "_x0"] = x0.numpy()
+        out[key + "_obs"] = obs.numpy()
+        out[key + "_vis"] = vis.numpy()
+        for k in ks:
+            solver = BFGSSolver(iterations=k, error_threshold=-1.0, minimum_step=-1.0).eval()
+            out[f"{key}_k{k}"] = solver(x0, fn).numpy()
+    np.savez_compressed(os.path.join(HERE, "ray_angle.npz"), **out)
+
+
 if __name__ == "__main__":
     torch.set_num_threads(8)
-    which = sys.argv[1:] or ["eval", "update", "ls", "traj"]
+    which = sys.argv[1:] or ["eval", "update", "ls", "traj", "ray"]
     if "eval" in which:
         gen_ba_eval()
     if "update" in which:
@@ -213,4 +268,6 @@ if __name__ == "__main__":
         gen_line_search()
     if "traj" in which:
         gen_trajectories()
+    if "ray" in which:
+        gen_ray_angle()
     print("golden fixtures written to", HERE)

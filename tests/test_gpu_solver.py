@@ -227,3 +227,66 @@ def test_global_vector_mode_equals_lds_mode(device, mode, monkeypatch):
     gv, _ = _gpu_solve(device, x0, obs, vis, 4, 256, True, **kw)
     monkeypatch.delenv("DAVA_FORCE_GV")
     assert _rel(gv, lds).max() <= TOL
+
+
+# ---- ray-angle residual (CalibrationNetwork's error, calibration_network.py:58-67) ----
+
+def _gpu_solve_ray(device, x0, obs, vis, m, n, **kw):
+    from deep_attention_visual_odometry_amd import BFGSSolver, RayAngleError
+
+    fn = RayAngleError(obs.to(device), vis.to(device), m, n)
+    s = BFGSSolver(**kw).eval()
+    out = s(x0.to(device), fn).cpu()
+    return out, s.last_status.cpu()
+
+
+@pytest.mark.parametrize("mode", ["dense", "compact"])
+@pytest.mark.parametrize("case,ks", [("c1", (5, 20, 100)), ("c2", (5, 20))])
+def test_ray_angle_golden_trajectories(device, case, ks, mode):
+    """Against BFGSSolver().eval() of the REAL reference on CalibrationNetwork's error
+    (tests/golden/ray_angle.npz).  The angle sum is not smooth where a residual vanishes,
+    so later iterates are more sensitive than the squared objective's: every K is held to
+    max(1e-5, 10 x the reference's own change under a 1-ulp nudge of x0)."""
+    g = np.load(os.path.join(GOLDEN, "ray_angle.npz"))
+    m, n = {"c1": (2, 64), "c2": (2, 128)}[case]
+    key = f"traj_{case}"
+    x0 = torch.tensor(g[key + "_x0"])
+    obs, vis = torch.tensor(g[key + "_obs"]), torch.tensor(g[key + "_vis"])
+    fn = objective.RayAngleClosure(obs, vis, m, n)
+    for k in ks:
+        out, status = _gpu_solve_ray(device, x0, obs, vis, m, n, iterations=k, error_threshold=-1.0,
+                                     minimum_step=-1.0, hessian_mode=mode)
+        ref = torch.tensor(g[f"{key}_k{k}"])
+        kw = dict(iterations=k, error_threshold=-1.0, minimum_step=-1.0)
+        nudged = solver.bfgs_solve(torch.nextafter(x0, torch.full_like(x0, float("inf"))), fn, **kw)
+        env = torch.clamp(10.0 * _rel(nudged, ref), min=TOL)
+        rel = _rel(out, ref)
+        assert (rel <= env).all(), (case, k, rel, env)
+        assert (status[:, 0] == k).all()
+
+
+def test_ray_angle_fixed_iterations_match_oracle_c3_shape(device):
+    from deep_attention_visual_odometry_amd import make_scenes
+
+    s = make_scenes(2, 4, 256, seed=331, drop=0.1, ray_angle=True)
+    x0, obs, vis = torch.tensor(s.initial), torch.tensor(s.observations), torch.tensor(s.visibility)
+    fn = objective.RayAngleClosure(obs, vis, 4, 256)
+    kw = dict(iterations=10, error_threshold=-1.0, minimum_step=-1.0)
+    ref = solver.bfgs_solve(x0, fn, **kw)
+    for mode in ("dense", "compact"):
+        out, _ = _gpu_solve_ray(device, x0, obs, vis, 4, 256, hessian_mode=mode, **kw)
+        assert _rel(out, ref).max() <= TOL, (mode, _rel(out, ref))
+
+
+def test_ray_angle_converges_from_noisy_guess(device):
+    """CalibrationNetwork's solver settings (error_threshold 1e-7, else defaults): the angle
+    sum falls by orders of magnitude, like the oracle's."""
+    from deep_attention_visual_odometry_amd import make_scenes
+
+    s = make_scenes(4, 2, 64, seed=332, ray_angle=True)
+    x0, obs, vis = torch.tensor(s.initial), torch.tensor(s.observations), torch.tensor(s.visibility)
+    out, status = _gpu_solve_ray(device, x0, obs, vis, 2, 64, error_threshold=1e-7, iterations=200)
+    e0 = objective.ray_angle_error(x0.double(), obs.double(), vis, 2, 64)
+    e1 = objective.ray_angle_error(out.double(), obs.double(), vis, 2, 64)
+    assert (e1 < 1e-2 * e0).all(), (e0, e1)
+    assert torch.isfinite(out).all()

@@ -45,7 +45,7 @@ def test_python_binding_types_every_declared_symbol():
 
 def test_library_is_built_for_gfx950(lib):
     assert lib.dava_device_arch() == b"gfx950"
-    assert lib.dava_abi_version() == 1
+    assert lib.dava_abi_version() == 2
     blob = open(lib._name, "rb").read()
     assert b"gfx950" in blob
 
@@ -67,6 +67,10 @@ def test_invalid_arguments_are_rejected_without_a_device(lib):
     assert lib.dava_ba_evaluate(ctypes.byref(wrong_p), None, None, None, None, None, None, None) == 1
     empty = N.DavaScene(0, 2, 16, 0, 3 + 48 + 6, None, None)
     assert lib.dava_ba_solve(ctypes.byref(empty), ctypes.byref(cfg), None, None, None, None, None, 0, None) == 0
+    bad_residual = N.DavaScene(0, 2, 16, 0, 3 + 48 + 6, None, None, 7)
+    assert lib.dava_ba_solve(ctypes.byref(bad_residual), ctypes.byref(cfg), None, None, None, None, None, 0, None) == 1
+    ray_distorted = N.DavaScene(0, 2, 16, 1, 3 + 48 + 6 + 5, None, None, N.DAVA_RESIDUAL_RAY_ANGLE)
+    assert lib.dava_ba_solve(ctypes.byref(ray_distorted), ctypes.byref(cfg), None, None, None, None, None, 0, None) == 4
     assert lib.dava_bfgs_update_inverse_hessian_f32(-1, 3, None, None, None, None, None) == 1
     assert lib.dava_bfgs_update_inverse_hessian_f64(0, 3, None, None, None, None, None) == 0
 

@@ -94,3 +94,29 @@ def test_bfgs_textbook_kat():
     right = torch.eye(3, dtype=torch.float64) - (y[:, None] * s[None, :]) / c
     expected = left @ h @ right + s[:, None] * s[None, :] / c
     assert torch.isclose(expected, solver.bfgs_update(h, s, y)).all()
+
+
+@pytest.mark.parametrize("shape", list(SHAPES))
+@pytest.mark.parametrize("dt", ["f64", "f32"])
+def test_ray_angle_objective_matches_reference_bitwise(shape, dt):
+    """CalibrationNetwork's error (calibration_network.py:58-67) and its autograd gradient."""
+    g = _load("ray_angle.npz")
+    m, n = SHAPES[shape]
+    key = f"eval_{shape}_{dt}"
+    x = torch.tensor(g[key + "_x"]).requires_grad_(True)
+    e = objective.ray_angle_error(x, torch.tensor(g[key + "_obs"]), torch.tensor(g[key + "_vis"]), m, n)
+    (grad,) = torch.autograd.grad(e.sum(), x)
+    assert np.array_equal(e.detach().numpy(), g[key + "_err"])
+    assert np.array_equal(grad.numpy(), g[key + "_grad"])
+
+
+@pytest.mark.parametrize("case,ks", [("c1", (5, 20, 100)), ("c2", (5, 20))])
+def test_ray_angle_trajectories_match_reference_bitwise(case, ks):
+    g = _load("ray_angle.npz")
+    m, n = SHAPES[case]
+    key = f"traj_{case}"
+    x0 = torch.tensor(g[key + "_x0"])
+    fn = objective.RayAngleClosure(torch.tensor(g[key + "_obs"]), torch.tensor(g[key + "_vis"]), m, n)
+    for k in ks:
+        out = solver.bfgs_solve(x0, fn, iterations=k, error_threshold=-1.0, minimum_step=-1.0)
+        assert np.array_equal(out.numpy(), g[f"{key}_k{k}"]), f"{case} K={k}"
