@@ -69,6 +69,10 @@ for _t in ("f32", "f64"):
     _scalar = ctypes.c_float if _t == "f32" else ctypes.c_double
     SIGNATURES.update({
         f"dava_bfgs_update_inverse_hessian_{_t}": (ctypes.c_int, [_c_i64, _c_i64, _vp, _vp, _vp, _vp, _vp]),
+        f"dava_bfgs_update_inverse_hessian_backward_{_t}": (ctypes.c_int, [_c_i64, _c_i64] + [_vp] * 8),
+        f"dava_bfgs_initial_scale_backward_{_t}": (ctypes.c_int, [_c_i64, _c_i64] + [_vp] * 6),
+        f"dava_bfgs_scale_matrix_backward_{_t}": (ctypes.c_int, [_c_i64, _c_i64] + [_vp] * 6),
+        f"dava_bfgs_search_direction_backward_{_t}": (ctypes.c_int, [_c_i64, _c_i64] + [_vp] * 6),
         f"dava_bfgs_initial_scale_{_t}": (ctypes.c_int, [_c_i64, _c_i64, _vp, _vp, _vp, _vp]),
         f"dava_bfgs_scale_matrix_{_t}": (ctypes.c_int, [_c_i64, _c_i64, _vp, _vp, _vp, _vp]),
         f"dava_bfgs_search_direction_{_t}": (ctypes.c_int, [_c_i64, _c_i64, _vp, _vp, _vp, _vp]),

@@ -14,9 +14,17 @@ contract, static methods and output conventions (functional, output
    state machine run in the library's HIP kernels.  The loop mirrors
    ``bfgs_solver.py:118-212`` including the mask contract of ``:99-104``.
 
-Not supported (raises rather than silently falling back): CPU tensors and
-differentiating through the solve (``parameters.requires_grad``; the
-reference's ``create_graph`` mode).
+Differentiating through the solve (``parameters.requires_grad``, the reference's
+``create_graph`` mode, ``:85, :134, :213-215``) runs the generic loop with the
+graph kept: the closure's gradient is taken with ``create_graph=True`` by
+PyTorch, and every solver op (initial scale, rescale, update, search direction)
+is an autograd node whose backward is a HIP kernel (csrc/bfgs_grad.hip); the
+line search is detached, as in the reference.  The fused objectives
+(:class:`ReprojectionError`, :class:`RayAngleError`) provide first derivatives
+only, so in that mode they must be replaced by a differentiable closure.
+
+Not supported (raises rather than silently falling back): CPU tensors, and
+second derivatives of the fused objectives.
 """
 from typing import Callable, Optional
 
@@ -76,16 +84,17 @@ class BFGSSolver(Module):
     def forward(self, parameters: torch.Tensor,
                 error_function: Callable[[torch.Tensor, torch.Tensor], torch.Tensor]) -> torch.Tensor:
         _native.require_device_tensor(parameters, "parameters")
-        if parameters.requires_grad:
+        if parameters.requires_grad and isinstance(error_function, ReprojectionError):
             raise NotImplementedError(
-                "differentiating through the solve (parameters.requires_grad, the reference's create_graph mode) "
-                "is not implemented on the GPU path yet; detach the initial guess")
+                "differentiating through the solve needs second derivatives of the error function; the fused "
+                "ReprojectionError / RayAngleError kernels provide first derivatives only -- pass a "
+                "differentiable closure (e.g. the reference's torch error_function) or detach the initial guess")
         if self.training:
             error_threshold, num_iterations = self.training_error_threshold, self.training_iterations
         else:
             error_threshold, num_iterations = self.error_threshold, self.iterations
         stochastic = self.training and (self.drop_path_p > 0.0 or self.return_second_last)
-        if isinstance(error_function, ReprojectionError) and not stochastic:
+        if isinstance(error_function, ReprojectionError) and not stochastic and not parameters.requires_grad:
             return self._fused(parameters, error_function, error_threshold, num_iterations)
         return self._generic(parameters, error_function, error_threshold, num_iterations)
 
@@ -134,7 +143,9 @@ class BFGSSolver(Module):
             mask[updating] = inner_mask
             return error_function(inner_parameters, mask)
 
-        parameters = parameters.detach()
+        create_graph = parameters.requires_grad  # bfgs_solver.py:85
+        if not create_graph:
+            parameters = parameters.detach()
         step = torch.zeros_like(parameters)
         error = torch.empty(batch_dimensions, dtype=parameters.dtype, device=device)
         gradient = torch.empty_like(parameters)
@@ -145,10 +156,12 @@ class BFGSSolver(Module):
             prev_gradient = gradient
             if self.training and self.drop_path_p > 0.0:
                 updating = updating & torch.greater(torch.rand_like(updating, dtype=torch.float32), self.drop_path_p)
-            upd_params = parameters[updating].requires_grad_(True)
+            upd_params = parameters[updating]
+            if not upd_params.requires_grad:
+                upd_params.requires_grad_(True)
             with torch.enable_grad():
                 upd_error = error_function(upd_params, updating)
-                (upd_grad,) = torch.autograd.grad(upd_error.sum(), upd_params)
+                (upd_grad,) = torch.autograd.grad(upd_error.sum(), upd_params, create_graph=create_graph)
             error = error.masked_scatter(updating, upd_error.detach())
             gradient = gradient.masked_scatter(updating.unsqueeze(-1).expand_as(gradient), upd_grad)
             updating = updating & torch.greater(error, error_threshold)
@@ -182,4 +195,4 @@ class BFGSSolver(Module):
                 break
             if self.training and self.return_second_last:
                 parameters = parameters.masked_scatter(updating.unsqueeze(-1).expand_as(parameters), new_params)
-        return parameters.detach()
+        return parameters if create_graph else parameters.detach()

@@ -96,8 +96,15 @@ def solve_workspace_bytes(batch: int, num_views: int, num_points: int, distortio
 
 
 # ---- generic BFGS building blocks ----
+# Each public op is a torch.autograd.Function whose forward AND backward are HIP kernels
+# (bfgs_ops.hip / bfgs_grad.hip), so the drop-in solver can be differentiated through
+# exactly like the reference (bfgs_solver.py:85, :134, :213-215).
 
-def update_inverse_hessian(h: torch.Tensor, s: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
+def _empty_or_none(needed: bool, like: torch.Tensor) -> Optional[torch.Tensor]:
+    return torch.empty_like(like) if needed else None
+
+
+def _update_forward(h: torch.Tensor, s: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
     lib = N.load_library()
     N.require_device_tensor(h, "inverse_hessian")
     n = h.shape[-1]
@@ -111,8 +118,36 @@ def update_inverse_hessian(h: torch.Tensor, s: torch.Tensor, y: torch.Tensor) ->
     return out.reshape(lead + (n, n))
 
 
-def initial_scale(s: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
-    """(..., 1) like the reference's keepdims result."""
+class _UpdateInverseHessian(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, h, s, y):
+        ctx.save_for_backward(h, s, y)
+        return _update_forward(h, s, y)
+
+    @staticmethod
+    @torch.autograd.function.once_differentiable
+    def backward(ctx, grad):
+        h, s, y = ctx.saved_tensors
+        n = h.shape[-1]
+        hb, sb, yb = _c(h).reshape(-1, n, n), _c(s).reshape(-1, n), _c(y).reshape(-1, n)
+        gb = _c(grad).reshape(-1, n, n)
+        gh = _empty_or_none(ctx.needs_input_grad[0], hb)
+        gs = _empty_or_none(ctx.needs_input_grad[1], sb)
+        gy = _empty_or_none(ctx.needs_input_grad[2], yb)
+        with torch.cuda.device(h.device):
+            N.check(getattr(N.load_library(), f"dava_bfgs_update_inverse_hessian_backward_{_dt(h)}")(
+                hb.shape[0], n, N.ptr(hb), N.ptr(sb), N.ptr(yb), N.ptr(gb), N.ptr(gh), N.ptr(gs), N.ptr(gy),
+                N.stream_of(h.device)), "dava_bfgs_update_inverse_hessian_backward")
+        return (gh.reshape(h.shape) if gh is not None else None, gs.reshape(s.shape) if gs is not None else None,
+                gy.reshape(y.shape) if gy is not None else None)
+
+
+def update_inverse_hessian(h: torch.Tensor, s: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
+    """``BFGSSolver.update_inverse_hessian`` (bfgs_solver.py:235-303), differentiable."""
+    return _UpdateInverseHessian.apply(h, s, y)
+
+
+def _initial_scale_forward(s: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
     lib = N.load_library()
     N.require_device_tensor(s, "step")
     n = s.shape[-1]
@@ -124,7 +159,34 @@ def initial_scale(s: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
     return out.reshape(s.shape[:-1] + (1,))
 
 
-def scale_matrix(scale: torch.Tensor, h: torch.Tensor) -> torch.Tensor:
+class _InitialScale(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, s, y):
+        ctx.save_for_backward(s, y)
+        return _initial_scale_forward(s, y)
+
+    @staticmethod
+    @torch.autograd.function.once_differentiable
+    def backward(ctx, grad):
+        s, y = ctx.saved_tensors
+        n = s.shape[-1]
+        sb, yb = _c(s).reshape(-1, n), _c(y).reshape(-1, n)
+        gb = _c(grad).reshape(-1)
+        gs = _empty_or_none(ctx.needs_input_grad[0], sb)
+        gy = _empty_or_none(ctx.needs_input_grad[1], yb)
+        with torch.cuda.device(s.device):
+            N.check(getattr(N.load_library(), f"dava_bfgs_initial_scale_backward_{_dt(s)}")(
+                sb.shape[0], n, N.ptr(sb), N.ptr(yb), N.ptr(gb), N.ptr(gs), N.ptr(gy), N.stream_of(s.device)),
+                "dava_bfgs_initial_scale_backward")
+        return (gs.reshape(s.shape) if gs is not None else None, gy.reshape(y.shape) if gy is not None else None)
+
+
+def initial_scale(s: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
+    """(..., 1) like the reference's keepdims result (bfgs_solver.py:217-233), differentiable."""
+    return _InitialScale.apply(s, y)
+
+
+def _scale_matrix_forward(scale: torch.Tensor, h: torch.Tensor) -> torch.Tensor:
     lib = N.load_library()
     n = h.shape[-1]
     hb = _c(h.detach()).reshape(-1, n, n)
@@ -136,7 +198,33 @@ def scale_matrix(scale: torch.Tensor, h: torch.Tensor) -> torch.Tensor:
     return out.reshape(h.shape)
 
 
-def search_direction(h: torch.Tensor, g: torch.Tensor) -> torch.Tensor:
+class _ScaleMatrix(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, scale, h):
+        ctx.save_for_backward(scale, h)
+        return _scale_matrix_forward(scale, h)
+
+    @staticmethod
+    @torch.autograd.function.once_differentiable
+    def backward(ctx, grad):
+        scale, h = ctx.saved_tensors
+        n = h.shape[-1]
+        hb, sc, gb = _c(h).reshape(-1, n, n), _c(scale).reshape(-1), _c(grad).reshape(-1, n, n)
+        gsc = _empty_or_none(ctx.needs_input_grad[0], sc)
+        gh = _empty_or_none(ctx.needs_input_grad[1], hb)
+        with torch.cuda.device(h.device):
+            N.check(getattr(N.load_library(), f"dava_bfgs_scale_matrix_backward_{_dt(h)}")(
+                hb.shape[0], n, N.ptr(sc), N.ptr(hb), N.ptr(gb), N.ptr(gsc), N.ptr(gh), N.stream_of(h.device)),
+                "dava_bfgs_scale_matrix_backward")
+        return (gsc.reshape(scale.shape) if gsc is not None else None, gh.reshape(h.shape) if gh is not None else None)
+
+
+def scale_matrix(scale: torch.Tensor, h: torch.Tensor) -> torch.Tensor:
+    """scale[..., None] * h: the k == 1 rescale of H0 (bfgs_solver.py:159-167), differentiable."""
+    return _ScaleMatrix.apply(scale, h)
+
+
+def _search_direction_forward(h: torch.Tensor, g: torch.Tensor) -> torch.Tensor:
     lib = N.load_library()
     n = h.shape[-1]
     hb = _c(h.detach()).reshape(-1, n, n)
@@ -146,6 +234,32 @@ def search_direction(h: torch.Tensor, g: torch.Tensor) -> torch.Tensor:
         N.check(getattr(lib, f"dava_bfgs_search_direction_{_dt(h)}")(
             hb.shape[0], n, N.ptr(hb), N.ptr(gb), N.ptr(out), N.stream_of(h.device)), "dava_bfgs_search_direction")
     return out.reshape(g.shape)
+
+
+class _SearchDirection(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, h, g):
+        ctx.save_for_backward(h, g)
+        return _search_direction_forward(h, g)
+
+    @staticmethod
+    @torch.autograd.function.once_differentiable
+    def backward(ctx, grad):
+        h, g = ctx.saved_tensors
+        n = h.shape[-1]
+        hb, gv, db = _c(h).reshape(-1, n, n), _c(g).reshape(-1, n), _c(grad).reshape(-1, n)
+        gh = _empty_or_none(ctx.needs_input_grad[0], hb)
+        gg = _empty_or_none(ctx.needs_input_grad[1], gv)
+        with torch.cuda.device(h.device):
+            N.check(getattr(N.load_library(), f"dava_bfgs_search_direction_backward_{_dt(h)}")(
+                hb.shape[0], n, N.ptr(hb), N.ptr(gv), N.ptr(db), N.ptr(gh), N.ptr(gg), N.stream_of(h.device)),
+                "dava_bfgs_search_direction_backward")
+        return (gh.reshape(h.shape) if gh is not None else None, gg.reshape(g.shape) if gg is not None else None)
+
+
+def search_direction(h: torch.Tensor, g: torch.Tensor) -> torch.Tensor:
+    """d = -H g (bfgs_solver.py:173-176), differentiable."""
+    return _SearchDirection.apply(h, g)
 
 
 class WolfeState:

@@ -175,6 +175,39 @@ int dava_wolfe_update_f32(int64_t batch, int32_t trial, float c1, float c2, int3
 int dava_wolfe_update_f64(int64_t batch, int32_t trial, double c1, double c2, int32_t strong, double* state,
                           uint8_t* flags, void* stream);
 
+/* ---- reverse mode of the building blocks (differentiating THROUGH the solve) ----
+ * The reference's create_graph mode (bfgs_solver.py:85, :134, :213-215) back-propagates
+ * through every op of the loop.  These are the vector-Jacobian products of the ops above;
+ * grad_out is dL/d(output), every grad_* output may be NULL (not formed).  All (batch,n,n)
+ * matrices are row-major and general (H is not assumed symmetric).                      */
+
+/* VJP of update_inverse_hessian, including InverseCurvature's custom backward
+ * (utils/func_inverse_curvature.py:36-51).  n <= 150 KiB / (9 sizeof(T)).               */
+int dava_bfgs_update_inverse_hessian_backward_f32(int64_t batch, int64_t n, const float* h, const float* s,
+                                                  const float* y, const float* grad_out, float* grad_h,
+                                                  float* grad_s, float* grad_y, void* stream);
+int dava_bfgs_update_inverse_hessian_backward_f64(int64_t batch, int64_t n, const double* h, const double* s,
+                                                  const double* y, const double* grad_out, double* grad_h,
+                                                  double* grad_s, double* grad_y, void* stream);
+
+/* VJP of initial_scale (clamp backward passes where the input >= the bound, as torch). */
+int dava_bfgs_initial_scale_backward_f32(int64_t batch, int64_t n, const float* s, const float* y,
+                                         const float* grad_out, float* grad_s, float* grad_y, void* stream);
+int dava_bfgs_initial_scale_backward_f64(int64_t batch, int64_t n, const double* s, const double* y,
+                                         const double* grad_out, double* grad_s, double* grad_y, void* stream);
+
+/* VJP of scale_matrix: grad_scale (batch), grad_h (batch,n,n). */
+int dava_bfgs_scale_matrix_backward_f32(int64_t batch, int64_t n, const float* scale, const float* h,
+                                        const float* grad_out, float* grad_scale, float* grad_h, void* stream);
+int dava_bfgs_scale_matrix_backward_f64(int64_t batch, int64_t n, const double* scale, const double* h,
+                                        const double* grad_out, double* grad_scale, double* grad_h, void* stream);
+
+/* VJP of search_direction (d = -H g): grad_h = -grad_d g^T, grad_g = -H^T grad_d. */
+int dava_bfgs_search_direction_backward_f32(int64_t batch, int64_t n, const float* h, const float* g,
+                                            const float* grad_d, float* grad_h, float* grad_g, void* stream);
+int dava_bfgs_search_direction_backward_f64(int64_t batch, int64_t n, const double* h, const double* g,
+                                            const double* grad_d, double* grad_h, double* grad_g, void* stream);
+
 /* ---- misc ---- */
 const char* dava_status_string(int status);
 int dava_abi_version(void);

@@ -160,8 +160,12 @@ def bfgs_solve(
     trajectory: Optional[list] = None,
 ) -> torch.Tensor:
     """Eval-mode ``BFGSSolver.forward`` (``bfgs_solver.py:80-215``).
-    ``trajectory`` (optional list) receives x after every iteration's step."""
-    x = x0.detach()
+    ``trajectory`` (optional list) receives x after every iteration's step.
+    When ``x0.requires_grad`` the solve is differentiable like the reference's
+    (``create_graph`` mode, ``:85, :129-135, :213-215``): the closure's gradient keeps its
+    graph and x stays attached; the line search is detached as in the reference."""
+    create_graph = x0.requires_grad
+    x = x0 if create_graph else x0.detach()
     shape = x.shape[:-1]
     p = x.size(-1)
     active = torch.ones(shape, dtype=torch.bool)
@@ -183,10 +187,11 @@ def bfgs_solve(
     for k in range(iterations):
         grad_prev = grad
         xa = x[active]
-        xa.requires_grad_(True)
+        if not xa.requires_grad:
+            xa.requires_grad_(True)
         with torch.enable_grad():
             fa = closure(xa, active)
-            (ga,) = torch.autograd.grad(fa.sum(), xa)
+            (ga,) = torch.autograd.grad(fa.sum(), xa, create_graph=create_graph)
         calls[0] += 1
         err = err.masked_scatter(active, fa.detach())
         grad = grad.masked_scatter(active.unsqueeze(-1).expand_as(grad), ga)
@@ -228,4 +233,4 @@ def bfgs_solve(
         record.iterations = steps_taken
         record.reason = reason
         record.closure_calls = calls[0]
-    return x.detach()
+    return x if create_graph else x.detach()

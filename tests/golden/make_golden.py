@@ -31,6 +31,12 @@ Fixtures written:
                           with its autograd gradient (fp64, fp32; C1/C2/C3 shapes at
                           B = 1), and BFGSSolver(...).eval() results on it after K in
                           {5, 20} (C1, C2 shapes) and K = 100 (C1).
+* ``solve_grad.npz``  -- gradients THROUGH ``BFGSSolver.forward`` (the reference's
+                          create_graph mode, bfgs_solver.py:85,134,213-215): d loss / d x0
+                          for the reference test's log-square function
+                          (test_bfgs_solver.py:263-273), a fixed-K Rosenbrock batch,
+                          and a small BA problem whose closure also captures the
+                          observations (d loss / d obs), fp64.
 * ``bfgs_traj.npz``   -- ``BFGSSolver(...).eval()`` results after K in
                           {5, 20, 100} iterations (error_threshold = -1,
                           minimum_step = -1) for C1 (2x64), C2 (2x128) and
@@ -257,9 +263,49 @@ def gen_ray_angle():
     np.savez_compressed(os.path.join(HERE, "ray_angle.npz"), **out)
 
 
+def gen_solve_grad():
+    out = {}
+    # the reference test's setup (test_bfgs_solver.py:263-273): log(1 + |x|^2), defaults + 1e-6
+    rng = np.random.default_rng(8101)
+    x0 = torch.tensor(rng.normal(0.0, 1.0, size=(3, 4)), requires_grad=True)
+    # .eval(): the reference test leaves the module in training mode (drop-path RNG); the
+    # golden pins the deterministic eval-mode graph
+    res = BFGSSolver(error_threshold=1e-6).eval()(x0, lambda x, _: (x.square().sum(dim=-1) + 1.0).log())
+    res.square().sum().backward()
+    out["log_x0"], out["log_out"], out["log_grad"] = x0.detach().numpy(), res.detach().numpy(), x0.grad.numpy()
+    # Rosenbrock, fixed K, a random linear loss
+    x0 = torch.tensor(rng.normal(0.0, 1.0, size=(4, 2)) + np.array([0.5, 0.5]), requires_grad=True)
+    w = torch.tensor(rng.normal(size=(4, 2)))
+
+    def rosen(p, _):
+        return (1.0 - p[..., 0]).square() + 100.0 * (p[..., 1] - p[..., 0].square()).square()
+
+    res = BFGSSolver(iterations=10, error_threshold=-1.0, minimum_step=-1.0).eval()(x0, rosen)
+    (res * w).sum().backward()
+    out["rosen_x0"], out["rosen_w"] = x0.detach().numpy(), w.numpy()
+    out["rosen_out"], out["rosen_grad"] = res.detach().numpy(), x0.grad.numpy()
+    # small BA problem (2 views x 8 points), closure captures observations that need grad
+    m, n = 2, 8
+    s = make_scenes(2, m, n, seed=8102)
+    x0 = torch.tensor(s.initial, dtype=torch.float64, requires_grad=True)
+    obs = torch.tensor(s.observations, dtype=torch.float64, requires_grad=True)
+    vis = torch.tensor(s.visibility)
+    w = torch.tensor(rng.normal(size=x0.shape))
+
+    def ba(p, mask):
+        return ref_objective(p, obs[mask], vis[mask], m, n)
+
+    res = BFGSSolver(iterations=5, error_threshold=-1.0, minimum_step=-1.0).eval()(x0, ba)
+    (res * w).sum().backward()
+    out["ba_x0"], out["ba_obs"], out["ba_vis"], out["ba_w"] = (x0.detach().numpy(), obs.detach().numpy(),
+                                                                vis.numpy(), w.numpy())
+    out["ba_out"], out["ba_grad"], out["ba_obs_grad"] = res.detach().numpy(), x0.grad.numpy(), obs.grad.numpy()
+    np.savez_compressed(os.path.join(HERE, "solve_grad.npz"), **out)
+
+
 if __name__ == "__main__":
     torch.set_num_threads(8)
-    which = sys.argv[1:] or ["eval", "update", "ls", "traj", "ray"]
+    which = sys.argv[1:] or ["eval", "update", "ls", "traj", "ray", "grad"]
     if "eval" in which:
         gen_ba_eval()
     if "update" in which:
@@ -270,4 +316,6 @@ if __name__ == "__main__":
         gen_trajectories()
     if "ray" in which:
         gen_ray_angle()
+    if "grad" in which:
+        gen_solve_grad()
     print("golden fixtures written to", HERE)

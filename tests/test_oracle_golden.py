@@ -120,3 +120,34 @@ def test_ray_angle_trajectories_match_reference_bitwise(case, ks):
     for k in ks:
         out = solver.bfgs_solve(x0, fn, iterations=k, error_threshold=-1.0, minimum_step=-1.0)
         assert np.array_equal(out.numpy(), g[f"{key}_k{k}"]), f"{case} K={k}"
+
+
+def test_gradient_through_the_solve_matches_reference_bitwise():
+    """The reference's create_graph mode (bfgs_solver.py:85,134,213-215; its test
+    test_bfgs_solver.py:263-273): d loss / d x0 (and d loss / d obs for a closure that
+    captures the observations) equal the reference's own autograd result."""
+    g = _load("solve_grad.npz")
+    x0 = torch.tensor(g["log_x0"]).requires_grad_(True)
+    out = solver.bfgs_solve(x0, lambda x, _: (x.square().sum(dim=-1) + 1.0).log(), error_threshold=1e-6)
+    out.square().sum().backward()
+    assert np.array_equal(out.detach().numpy(), g["log_out"])
+    assert np.array_equal(x0.grad.numpy(), g["log_grad"])
+    assert (x0.grad.abs() > 0).all()
+
+    x0 = torch.tensor(g["rosen_x0"]).requires_grad_(True)
+
+    def rosen(p, _):
+        return (1.0 - p[..., 0]).square() + 100.0 * (p[..., 1] - p[..., 0].square()).square()
+
+    out = solver.bfgs_solve(x0, rosen, iterations=10, error_threshold=-1.0, minimum_step=-1.0)
+    (out * torch.tensor(g["rosen_w"])).sum().backward()
+    assert np.array_equal(x0.grad.numpy(), g["rosen_grad"])
+
+    x0 = torch.tensor(g["ba_x0"]).requires_grad_(True)
+    obs = torch.tensor(g["ba_obs"]).requires_grad_(True)
+    fn = objective.ReprojectionClosure(obs, torch.tensor(g["ba_vis"]), 2, 8)
+    out = solver.bfgs_solve(x0, fn, iterations=5, error_threshold=-1.0, minimum_step=-1.0)
+    (out * torch.tensor(g["ba_w"])).sum().backward()
+    assert np.array_equal(out.detach().numpy(), g["ba_out"])
+    assert np.array_equal(x0.grad.numpy(), g["ba_grad"])
+    assert np.array_equal(obs.grad.numpy(), g["ba_obs_grad"])
