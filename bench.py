@@ -47,6 +47,8 @@ def parse():
     p.add_argument("--no-distortion", action="store_true")
     p.add_argument("--iterations", type=int, default=100)
     p.add_argument("--mode", choices=["dense", "compact"], default="compact")
+    p.add_argument("--residual", choices=["reprojection", "ray_angle"], default="reprojection",
+                   help="ray_angle: CalibrationNetwork's error (pinhole only; not the headline metric)")
     p.add_argument("--seed", type=int, default=20251015 + 3000)
     p.add_argument("--cpu-sample", type=int, default=12, help="problems timed on the CPU oracle (0 = skip)")
     p.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "pmc_traffic.json"))
@@ -81,7 +83,10 @@ def cpu_baseline(args, x0, obs, vis, p):
     from oracle import objective, solver
 
     n = min(args.cpu_sample, x0.shape[0])
-    fn = objective.ReprojectionClosure(obs[:n], vis[:n], args.views, args.points, not args.no_distortion)
+    if args.residual == "ray_angle":
+        fn = objective.RayAngleClosure(obs[:n], vis[:n], args.views, args.points)
+    else:
+        fn = objective.ReprojectionClosure(obs[:n], vis[:n], args.views, args.points, not args.no_distortion)
     threads = torch.get_num_threads()
     t = time.perf_counter()
     solver.bfgs_solve(x0[:n], fn, iterations=args.iterations, error_threshold=-1.0, minimum_step=-1.0)
@@ -91,7 +96,7 @@ def cpu_baseline(args, x0, obs, vis, p):
         "unit": "problems/s",
         "cores": threads,
         "kind": "port",
-        "sample": f"{n} problems of the same C3 workload (first {n} of rank 0's batch), K={args.iterations}, "
+        "sample": f"{n} problems of the same workload (first {n} of rank 0's batch), K={args.iterations}, "
                   f"oracle = PyTorch-CPU restatement bitwise-equal to the reference, {threads} torch threads, "
                   f"{dt:.1f} s",
     }
@@ -112,15 +117,19 @@ def main():
     from deep_attention_visual_odometry_amd.sharding import gather_rows, shard_range
 
     distortion = not args.no_distortion
+    ray = args.residual == "ray_angle"
+    if ray and distortion:
+        raise SystemExit("--residual ray_angle is pinhole only: add --no-distortion")
+    residual = _native.DAVA_RESIDUAL_RAY_ANGLE if ray else _native.DAVA_RESIDUAL_SQUARED_REPROJECTION
     b = args.batch
     first = shard_range(world * b, world, rank).start  # this rank's slab of the global batch
-    cache = f"/tmp/dava_scenes_{args.seed}_{first}_{b}_{args.views}_{args.points}_{int(distortion)}.npz"
+    cache = f"/tmp/dava_scenes_{args.seed}_{first}_{b}_{args.views}_{args.points}_{int(distortion)}_{int(ray)}.npz"
     if os.path.exists(cache):  # generation is ~1 ms/problem on the host; cache it for repeated runs
         z = np.load(cache)
         scenes = type("S", (), {k: z[k] for k in ("initial", "observations", "visibility")})
     else:
         scenes = make_scenes(b, args.views, args.points, distortion=distortion, seed=args.seed,
-                             first_index=first)
+                             first_index=first, ray_angle=ray)
         np.savez(cache, initial=scenes.initial, observations=scenes.observations, visibility=scenes.visibility)
     x0_cpu = torch.tensor(scenes.initial)
     obs_cpu = torch.tensor(scenes.observations)
@@ -144,7 +153,8 @@ def main():
             e0.record(stream)
         x, _, status = native_ops.ba_solve(x0, obs, vis, args.views, args.points, distortion,
                                            iterations=args.iterations, error_threshold=-1.0, minimum_step=-1.0,
-                                           hessian_mode=mode, want_status=True, workspace=workspace)
+                                           hessian_mode=mode, want_status=True, workspace=workspace,
+                                           residual=residual)
         if timed:
             e1.record(stream)
             kernel_ms.append((e0, e1))
@@ -179,6 +189,7 @@ def main():
     finite = bool(torch.isfinite(x).all().item())
 
     if rank == 0:
+        headline = (b, args.views, args.points, distortion, ray, args.iterations) == (8192, 4, 256, True, False, 100)
         value = world * b * args.steps / elapsed
         algo = b * (dense_algorithmic_bytes if args.mode == "dense" else compact_algorithmic_bytes)(
             p, mn, args.iterations)
@@ -190,6 +201,8 @@ def main():
                 with open(args.traffic_json) as fh:
                     tj = json.load(fh)
                 key = f"{args.mode}_B{b}_M{args.views}_N{args.points}_D{int(distortion)}_K{args.iterations}"
+                if ray:
+                    key += "_ray"
                 if key in tj:
                     traffic = tj[key]["hbm_bytes_per_launch"]
             except (OSError, ValueError, KeyError):
@@ -201,7 +214,8 @@ def main():
         cpu = cpu_baseline(args, x0_cpu, obs_cpu, vis_cpu, p) if (world == 1 and args.cpu_sample > 0) else None
         line = {
             "metric": f"BA problems/sec (B={b} per GPU, {args.views} views x {args.points} pts"
-                      f"{', Brown-Conrady' if distortion else ''}, K={args.iterations} BFGS iterations)",
+                      f"{', Brown-Conrady' if distortion else ''}{', ray-angle residual' if ray else ''}, "
+                      f"K={args.iterations} BFGS iterations)",
             "value": round(value, 2),
             "unit": "problems/s",
             "n_gpus": world,
@@ -214,9 +228,10 @@ def main():
             "dtype": "f32",
             "data": "synthetic (seeded look-at scenes, noise-free observations, x0 = truth + noise)",
             "config": {
-                "workload": ("C3" if world == 1 else f"C4-style dp{world}") +
+                "workload": (("C3" if world == 1 else f"C4-style dp{world}") if headline else "custom") +
                             f": batch={b} per GPU, {args.views} views x {args.points} pts, "
-                            f"{'pinhole+Brown-Conrady' if distortion else 'pinhole'}, P={p}, "
+                            f"{'pinhole+Brown-Conrady' if distortion else 'pinhole'}"
+                            f"{' ray-angle residual' if ray else ''}, P={p}, "
                             f"K={args.iterations} fixed iterations, strong Wolfe (c1=1e-4, c2=0.9)",
                 "global_batch": world * b,
                 "num_parameters": p,
