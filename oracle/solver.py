@@ -158,12 +158,20 @@ def bfgs_solve(
     minimum_step: float = 1e-8,
     record: Optional[SolveRecord] = None,
     trajectory: Optional[list] = None,
+    training: bool = False,
+    drop_path_p: float = 0.0,
+    return_second_last: bool = False,
 ) -> torch.Tensor:
     """Eval-mode ``BFGSSolver.forward`` (``bfgs_solver.py:80-215``).
     ``trajectory`` (optional list) receives x after every iteration's step.
     When ``x0.requires_grad`` the solve is differentiable like the reference's
     (``create_graph`` mode, ``:85, :129-135, :213-215``): the closure's gradient keeps its
-    graph and x stays attached; the line search is detached as in the reference."""
+    graph and x stays attached; the line search is detached as in the reference.
+    ``training=True`` adds the training-mode semantics (the caller passes the training
+    threshold / iteration count): per-iteration drop-path ``active &= rand_like > p``
+    (``:121-125``, drawn with ``torch.rand_like`` so a test can make it deterministic) and
+    ``return_second_last`` (``:196-212``), including the reference's scatter of the
+    previous active set's rows into the smaller new active set."""
     create_graph = x0.requires_grad
     x = x0 if create_graph else x0.detach()
     shape = x.shape[:-1]
@@ -186,6 +194,8 @@ def bfgs_solve(
     reason = torch.full(shape, STOP_ITERATIONS, dtype=torch.int32)
     for k in range(iterations):
         grad_prev = grad
+        if training and drop_path_p > 0.0:
+            active = active & torch.greater(torch.rand_like(active, dtype=torch.float32), drop_path_p)
         xa = x[active]
         if not xa.requires_grad:
             xa.requires_grad_(True)
@@ -220,7 +230,8 @@ def bfgs_solve(
         )
         s = alpha.unsqueeze(-1) * d
         step = step.masked_scatter(active.unsqueeze(-1).expand_as(step), s)
-        x = x.masked_scatter(active.unsqueeze(-1).expand_as(x), xa + s)
+        if not (training and return_second_last):
+            x = x.masked_scatter(active.unsqueeze(-1).expand_as(x), xa + s)
         steps_taken[active] += 1
         if trajectory is not None:
             trajectory.append(x.detach().clone())
@@ -229,6 +240,8 @@ def bfgs_solve(
         active = still
         if not active.any():
             break
+        if training and return_second_last:
+            x = x.masked_scatter(active.unsqueeze(-1).expand_as(x), xa + s)
     if record is not None:
         record.iterations = steps_taken
         record.reason = reason

@@ -37,6 +37,11 @@ Fixtures written:
                           (test_bfgs_solver.py:263-273), a fixed-K Rosenbrock batch,
                           and a small BA problem whose closure also captures the
                           observations (d loss / d obs), fp64.
+* ``training.npz``    -- ``BFGSSolver`` in TRAINING mode (bfgs_solver.py:88-93, :121-125,
+                          :196-212): training threshold / iteration count, drop-path and
+                          return_second_last, with ``torch.rand_like`` replaced by a seeded
+                          CPU stream (``deterministic_rand_like``) so the run is
+                          reproducible; the same replacement is applied in the parity tests.
 * ``bfgs_traj.npz``   -- ``BFGSSolver(...).eval()`` results after K in
                           {5, 20, 100} iterations (error_threshold = -1,
                           minimum_step = -1) for C1 (2x64), C2 (2x128) and
@@ -75,6 +80,9 @@ from deep_attention_visual_odometry.geometry import (  # noqa: E402
 )
 
 from deep_attention_visual_odometry_amd.scenes import make_scenes  # noqa: E402
+
+sys.path.insert(0, os.path.dirname(HERE))
+from rng_patch import deterministic_rand_like  # noqa: E402
 
 SHAPES = {"c1": (2, 64), "c2": (2, 128), "c3": (4, 256)}
 
@@ -303,9 +311,43 @@ def gen_solve_grad():
     np.savez_compressed(os.path.join(HERE, "solve_grad.npz"), **out)
 
 
+TRAINING_CASES = {
+    # name: (solver kwargs, seed)
+    "rosen_drop": (dict(drop_path_p=0.3, training_iterations=30, training_error_threshold=1e-3), 9101),
+    "rosen_second_last": (dict(drop_path_p=0.0, return_second_last=True, training_iterations=40,
+                               training_error_threshold=1e-6), 9102),
+    "rosen_both": (dict(drop_path_p=0.2, return_second_last=True, training_iterations=25), 9103),
+}
+
+
+def gen_training():
+    out = {}
+    rng = np.random.default_rng(9100)
+    x0 = torch.tensor(rng.normal(0.0, 1.0, size=(6, 2)) + np.array([0.5, 0.5]))
+    out["rosen_x0"] = x0.numpy()
+
+    def rosen(p, _):
+        return (1.0 - p[..., 0]).square() + 100.0 * (p[..., 1] - p[..., 0].square()).square()
+
+    for name, (kw, seed) in TRAINING_CASES.items():
+        solver = BFGSSolver(**kw)  # nn.Module default: training mode
+        assert solver.training
+        with deterministic_rand_like(seed):
+            out[name] = solver(x0, rosen).numpy()
+    # a BA batch with drop-path
+    m, n = SHAPES["c1"]
+    s, xb, obs, vis = scenes_as_tensors(4, m, n, 9200, torch.float32)
+    out["ba_x0"], out["ba_obs"], out["ba_vis"] = xb.numpy(), obs.numpy(), vis.numpy()
+    with deterministic_rand_like(9201):
+        out["ba_drop"] = BFGSSolver(drop_path_p=0.25, training_iterations=12,
+                                    training_error_threshold=-1.0, minimum_step=-1.0)(
+            xb, closure_for(obs, vis, m, n)).numpy()
+    np.savez_compressed(os.path.join(HERE, "training.npz"), **out)
+
+
 if __name__ == "__main__":
     torch.set_num_threads(8)
-    which = sys.argv[1:] or ["eval", "update", "ls", "traj", "ray", "grad"]
+    which = sys.argv[1:] or ["eval", "update", "ls", "traj", "ray", "grad", "train"]
     if "eval" in which:
         gen_ba_eval()
     if "update" in which:
@@ -318,4 +360,6 @@ if __name__ == "__main__":
         gen_ray_angle()
     if "grad" in which:
         gen_solve_grad()
+    if "train" in which:
+        gen_training()
     print("golden fixtures written to", HERE)

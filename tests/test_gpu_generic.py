@@ -392,3 +392,57 @@ def test_generic_path_with_native_objective_matches_fused(device):
     generic = BFGSSolver(iterations=20, error_threshold=-1.0, minimum_step=-1.0).eval()._generic(x0, fn, -1.0, 20)
     rel = (fused - generic).double().norm(dim=-1) / generic.double().norm(dim=-1)
     assert rel.max().item() <= 1e-5
+
+
+# ---- training-mode semantics (bfgs_solver.py:88-93, :121-125, :196-212) ----
+
+TRAINING = {
+    "rosen_drop": (dict(drop_path_p=0.3, training_iterations=30, training_error_threshold=1e-3), 9101),
+    "rosen_second_last": (dict(drop_path_p=0.0, return_second_last=True, training_iterations=40,
+                               training_error_threshold=1e-6), 9102),
+    "rosen_both": (dict(drop_path_p=0.2, return_second_last=True, training_iterations=25), 9103),
+}
+
+
+@pytest.mark.parametrize("case", list(TRAINING))
+def test_training_mode_matches_reference(device, case):
+    """The module's default training mode against the REAL reference (tests/golden/training.npz),
+    drop-path draws made deterministic by the same stand-in for torch.rand_like (fp64)."""
+    from deep_attention_visual_odometry_amd import BFGSSolver
+    from rng_patch import deterministic_rand_like
+
+    g = np.load(os.path.join(GOLDEN, "training.npz"))
+    kw, seed = TRAINING[case]
+    solver = BFGSSolver(**kw)
+    assert solver.training
+    with deterministic_rand_like(seed):
+        out = solver(torch.tensor(g["rosen_x0"], device=device), rosenbrock).cpu()
+    ref = torch.tensor(g[case])
+    assert ((out - ref).norm(dim=-1) / ref.norm(dim=-1)).max().item() < 1e-7  # fp64, reduction order only
+
+
+def test_training_mode_ba_drop_path_matches_reference(device):
+    from deep_attention_visual_odometry_amd import BFGSSolver
+    from oracle import objective
+
+    from rng_patch import deterministic_rand_like
+
+    g = np.load(os.path.join(GOLDEN, "training.npz"))
+    obs, vis = torch.tensor(g["ba_obs"], device=device), torch.tensor(g["ba_vis"], device=device)
+    fn = objective.ReprojectionClosure(obs, vis, 2, 64)
+    solver = BFGSSolver(drop_path_p=0.25, training_iterations=12, training_error_threshold=-1.0, minimum_step=-1.0)
+    with deterministic_rand_like(9201):
+        out = solver(torch.tensor(g["ba_x0"], device=device), fn).cpu()
+    ref = torch.tensor(g["ba_drop"])
+    assert ((out - ref).norm(dim=-1) / ref.norm(dim=-1)).max().item() < 1e-5
+
+
+def test_training_mode_uses_training_threshold_and_iterations(device):
+    from deep_attention_visual_odometry_amd import BFGSSolver
+
+    x0 = torch.tensor([[1.5, -2.0]], device=device)
+    solver = BFGSSolver(iterations=500, error_threshold=1e-12, training_iterations=3,
+                        training_error_threshold=1e-12, drop_path_p=0.0)
+    trained = solver(x0, rosenbrock)
+    evald = solver.eval()(x0, rosenbrock)
+    assert rosenbrock(evald).item() < rosenbrock(trained).item()

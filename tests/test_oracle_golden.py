@@ -151,3 +151,48 @@ def test_gradient_through_the_solve_matches_reference_bitwise():
     assert np.array_equal(out.detach().numpy(), g["ba_out"])
     assert np.array_equal(x0.grad.numpy(), g["ba_grad"])
     assert np.array_equal(obs.grad.numpy(), g["ba_obs_grad"])
+
+
+TRAINING = {
+    "rosen_drop": (dict(drop_path_p=0.3, training_iterations=30, training_error_threshold=1e-3), 9101),
+    "rosen_second_last": (dict(drop_path_p=0.0, return_second_last=True, training_iterations=40,
+                               training_error_threshold=1e-6), 9102),
+    "rosen_both": (dict(drop_path_p=0.2, return_second_last=True, training_iterations=25), 9103),
+}
+
+
+def _oracle_training(x0, fn, kw):
+    return solver.bfgs_solve(x0, fn, training=True, drop_path_p=kw.get("drop_path_p", 0.1),
+                             return_second_last=kw.get("return_second_last", False),
+                             iterations=kw.get("training_iterations", 1000),
+                             error_threshold=kw.get("training_error_threshold", 1e-4),
+                             minimum_step=kw.get("minimum_step", 1e-8))
+
+
+@pytest.mark.parametrize("case", list(TRAINING))
+def test_training_mode_matches_reference_bitwise(case):
+    """Training-mode semantics (bfgs_solver.py:88-93, :121-125, :196-212) with the drop-path
+    draws made deterministic (tests/rng_patch.py), including return_second_last's scatter
+    of the previous active rows into the new active set."""
+    from rng_patch import deterministic_rand_like
+
+    g = _load("training.npz")
+    kw, seed = TRAINING[case]
+
+    def rosen(p, _):
+        return (1.0 - p[..., 0]).square() + 100.0 * (p[..., 1] - p[..., 0].square()).square()
+
+    with deterministic_rand_like(seed):
+        out = _oracle_training(torch.tensor(g["rosen_x0"]), rosen, kw)
+    assert np.array_equal(out.numpy(), g[case])
+
+
+def test_training_mode_ba_drop_path_matches_reference_bitwise():
+    from rng_patch import deterministic_rand_like
+
+    g = _load("training.npz")
+    fn = objective.ReprojectionClosure(torch.tensor(g["ba_obs"]), torch.tensor(g["ba_vis"]), 2, 64)
+    kw = dict(drop_path_p=0.25, training_iterations=12, training_error_threshold=-1.0, minimum_step=-1.0)
+    with deterministic_rand_like(9201):
+        out = _oracle_training(torch.tensor(g["ba_x0"]), fn, kw)
+    assert np.array_equal(out.numpy(), g["ba_drop"])
