@@ -7,7 +7,10 @@ Drop-in for the hot path of jskinn/deep-attention-visual-odometry
 """
 from .autograd_solvers import BFGSSolver, line_search_wolfe_conditions
 from .camera_model import RayAngleError, ReprojectionError, num_parameters, unpack_calibration_parameters
+from .camera_model import PinholeCameraModelL1
+from .geometry import LieRotation
 from .scenes import make_scenes
+from .solvers import BFGSCameraSolver, IOptimisableFunction, LineSearchStrongWolfeConditions
 
 __all__ = [
     "BFGSSolver",
@@ -17,4 +20,10 @@ __all__ = [
     "num_parameters",
     "unpack_calibration_parameters",
     "make_scenes",
+    # legacy IOptimisableFunction path (solvers/, camera_model/pinhole_camera_model_l1.py)
+    "BFGSCameraSolver",
+    "IOptimisableFunction",
+    "LieRotation",
+    "LineSearchStrongWolfeConditions",
+    "PinholeCameraModelL1",
 ]

@@ -129,3 +129,6 @@ class RayAngleError(ReprojectionError):
 
     def __init__(self, observations: torch.Tensor, visibility: torch.Tensor, num_views: int, num_points: int):
         super().__init__(observations, visibility, num_views, num_points, distortion=False)
+
+
+from .pinhole_camera_model_l1 import PinholeCameraModelL1  # noqa: E402  (legacy IOptimisableFunction model)

@@ -208,6 +208,26 @@ int dava_bfgs_search_direction_backward_f32(int64_t batch, int64_t n, const floa
 int dava_bfgs_search_direction_backward_f64(int64_t batch, int64_t n, const double* h, const double* g,
                                             const double* grad_d, double* grad_h, double* grad_g, void* stream);
 
+/* ---- legacy IOptimisableFunction camera model (camera_model/pinhole_camera_model_l1.py) ----
+ * Error and/or the reference's hand-written gradient of PinholeCameraModelL1 for
+ * batch x estimates independent estimates (one workgroup each).  Per estimate:
+ *   focal, cx, cy (1)      translation, lie_vector (views, 3)     world_points (points-2, 3)
+ * shared per batch item: true_points (views, points, 2), visibility (views, points) 0/1.
+ * inverse_pixel_ratio = 1/|maximum_pixel_ratio|; error_scale = the reference's fp32
+ * sqrt(1/(views*points)).  error_out (batch, estimates), gradient_out (batch, estimates, P)
+ * with P = 3 + 6 views + 3 points - 7, either may be NULL.  points >= 3.                  */
+int dava_l1_camera_evaluate_f32(int64_t batch, int32_t estimates, int32_t views, int32_t points, const float* focal,
+                                const float* cx, const float* cy, const float* translation, const float* lie_vector,
+                                const float* world_points, const float* true_points, const uint8_t* visibility,
+                                float minimum_z_distance, float inverse_pixel_ratio, float max_gradient,
+                                float error_scale, float* error_out, float* gradient_out, void* stream);
+int dava_l1_camera_evaluate_f64(int64_t batch, int32_t estimates, int32_t views, int32_t points, const double* focal,
+                                const double* cx, const double* cy, const double* translation,
+                                const double* lie_vector, const double* world_points, const double* true_points,
+                                const uint8_t* visibility, double minimum_z_distance, double inverse_pixel_ratio,
+                                double max_gradient, double error_scale, double* error_out, double* gradient_out,
+                                void* stream);
+
 /* ---- misc ---- */
 const char* dava_status_string(int status);
 int dava_abi_version(void);

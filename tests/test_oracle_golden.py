@@ -196,3 +196,23 @@ def test_training_mode_ba_drop_path_matches_reference_bitwise():
     with deterministic_rand_like(9201):
         out = _oracle_training(torch.tensor(g["ba_x0"]), fn, kw)
     assert np.array_equal(out.numpy(), g["ba_drop"])
+
+
+@pytest.mark.parametrize("case", ["mg1e3", "default", "behind"])
+@pytest.mark.parametrize("dt", ["f64", "f32"])
+def test_camera_l1_error_and_gradient_match_reference_bitwise(case, dt):
+    """Legacy PinholeCameraModelL1 (camera_model/pinhole_camera_model_l1.py) get_error and its
+    hand-written get_gradient, max_gradient clipping and z clamping included."""
+    from oracle import camera_l1
+
+    g = _load("camera_l1.npz")
+    key = f"{case}_{dt}"
+    kw = {"mg1e3": dict(max_gradient=1e3), "default": dict(), "behind": dict(max_gradient=50.0,
+                                                                             minimum_z_distance=0.5)}[case]
+    args = [torch.tensor(g[f"{key}_{k}"]) for k in ("focal_length", "cx", "cy", "translation", "lie", "world",
+                                                      "true", "vis")]
+    ez = {k: v for k, v in kw.items() if k != "max_gradient"}
+    err = camera_l1.l1_error(*args, **ez)
+    grad = camera_l1.l1_gradient(*args, **kw)
+    assert np.array_equal(err.numpy(), g[key + "_error"])
+    assert np.array_equal(grad.numpy(), g[key + "_gradient"])
