@@ -25,6 +25,9 @@
 #pragma once
 
 #include "dava_common.hpp"
+#include "dava_dual.hpp"
+
+#include <type_traits>
 
 namespace dava {
 
@@ -37,28 +40,32 @@ struct Layout {
 };
 
 // ---- Taylor-branched ratios, same thresholds and series as the reference ----
-__device__ __forceinline__ float sinc(float x) {
-  if (fabsf(x) < 0.01f) {
-    const float x2 = x * x, x4 = x2 * x2, x6 = x4 * x2;
+// (templated on the scalar: float, or Dual for second derivatives, dava_dual.hpp)
+template <typename S>
+__device__ __forceinline__ S sinc(S x) {
+  if (fabs_(x) < 0.01f) {
+    const S x2 = x * x, x4 = x2 * x2, x6 = x4 * x2;
     return 1.0f - x2 / 6.0f + x4 / 120.0f - x6 / 5040.0f;
   }
-  return sinf(x) / x;
+  return sin_(x) / x;
 }
-__device__ __forceinline__ float sinc_slope(float x) {  // cos/x^2 - sin/x^3
-  const float x2 = x * x;
-  if (fabsf(x) < 0.01f) {
-    const float x4 = x2 * x2, x6 = x4 * x2;
+template <typename S>
+__device__ __forceinline__ S sinc_slope(S x) {  // cos/x^2 - sin/x^3
+  const S x2 = x * x;
+  if (fabs_(x) < 0.01f) {
+    const S x4 = x2 * x2, x6 = x4 * x2;
     return -1.0f / 3.0f + x2 / 30.0f - x4 / 840.0f + x6 / 45360.0f;
   }
-  return cosf(x) / x2 - sinf(x) / (x * x2);
+  return cos_(x) / x2 - sin_(x) / (x * x2);
 }
-__device__ __forceinline__ float versine_ratio(float x) {  // (1 - cos x)/x^2
-  const float x2 = x * x;
-  if (fabsf(x) < 0.05f) {
-    const float x4 = x2 * x2, x6 = x4 * x2;
+template <typename S>
+__device__ __forceinline__ S versine_ratio(S x) {  // (1 - cos x)/x^2
+  const S x2 = x * x;
+  if (fabs_(x) < 0.05f) {
+    const S x4 = x2 * x2, x6 = x4 * x2;
     return 0.5f - x2 / 24.0f + x4 / 720.0f - x6 / 40320.0f;
   }
-  return (1.0f - cosf(x)) / x2;
+  return (1.0f - cos_(x)) / x2;
 }
 
 // ---- per-view constants, kept in LDS (one row of kViewStride floats per view >= 1) ----
@@ -79,13 +86,14 @@ constexpr int kViewPart = 8;
 __host__ __device__ inline int views_floats(int M) { return (M - 1) * kViewStride; }
 __host__ __device__ inline int vpart_floats(int M) { return M * kWaves * kViewPart; }
 
+template <typename S>
 struct Intrinsics {
-  float f, cx, cy, k1, k2, k3, p1, p2;
+  S f, cx, cy, k1, k2, k3, p1, p2;
 };
 
-template <bool TRIAL>
-__device__ __forceinline__ float trial_value(const float* x, const float* d, float a, int i) {
-  if constexpr (TRIAL) return __fadd_rn(x[i], __fmul_rn(a, d[i]));
+template <bool TRIAL, typename S>
+__device__ __forceinline__ S trial_value(const S* x, const S* d, float a, int i) {
+  if constexpr (TRIAL) return fadd_rn(x[i], fmul_rn(S(a), d[i]));
   else return x[i];
 }
 
@@ -96,60 +104,62 @@ __device__ __forceinline__ float trial_value(const float* x, const float* d, flo
 // 2 atan2(|a^ - b^|, |a^ + b^|) with both norms clamped at 2^-52
 // (geometry/projective_plane_angle_distance.py:20-64).  Derivatives follow torch's
 // conventions: a zero norm has zero subgradient, a clamped norm passes none.
+template <typename S>
 struct RayAngle {
-  float cx, cy, F, Fp;  // principal point, focal elu(f) + 1 and its derivative
-  float dcx, dcy, dF;   // SLOPE: tangents
+  S cx, cy, F, Fp;  // principal point, focal elu(f) + 1 and its derivative
+  S dcx, dcy, dF;   // SLOPE: tangents
 };
 constexpr float kRayEps = 2.220446049250313e-16f;
 
 // unit vector x / clamp(|x|, eps) and the projection of a cotangent / tangent through it
-__device__ __forceinline__ void ray_unit_backward(float r, float n, const float (&u)[3], const float (&g)[3],
-                                                  float (&out)[3]) {
-  const float k = r >= kRayEps ? u[0] * g[0] + u[1] * g[1] + u[2] * g[2] : 0.0f;
+template <typename S>
+__device__ __forceinline__ void ray_unit_backward(S r, S n, const S (&u)[3], const S (&g)[3], S (&out)[3]) {
+  const S k = r >= kRayEps ? u[0] * g[0] + u[1] * g[1] + u[2] * g[2] : S(0.0f);
 #pragma unroll
   for (int c = 0; c < 3; ++c) out[c] = (g[c] - u[c] * k) / n;
 }
 
-template <bool GRAD, bool SLOPE>
-__device__ __forceinline__ void ray_angle_pair(const RayAngle& ra, const float* ob, uint8_t visible, float p0,
-                                               float p1, float p2, float dp0, float dp1, float dp2, float& e,
-                                               float& sl, float (&gin)[8], float& G0, float& G1, float& G2) {
+template <bool GRAD, bool SLOPE, typename S>
+__device__ __forceinline__ void ray_angle_pair(const RayAngle<S>& ra, const float* ob, uint8_t visible, S p0,
+                                               S p1, S p2, S dp0, S dp1, S dp2, S& e,
+                                               S& sl, S (&gin)[8], S& G0, S& G1, S& G2, S& go0, S& go1) {
   const float wgt = visible ? 1.0f : 0.0f;
-  const float h[3] = {ob[0] - ra.cx, ob[1] - ra.cy, ra.F};
-  const float hr = sqrtf(h[0] * h[0] + h[1] * h[1] + h[2] * h[2]);
-  const float hn = clamp_min(hr, kRayEps);
-  const float a[3] = {h[0] / hn, h[1] / hn, h[2] / hn};
-  const float pr = sqrtf(p0 * p0 + p1 * p1 + p2 * p2);
-  const float pn = clamp_min(pr, kRayEps);
-  const float b[3] = {p0 / pn, p1 / pn, p2 / pn};
-  const float su[3] = {a[0] + b[0], a[1] + b[1], a[2] + b[2]};
-  const float df[3] = {a[0] - b[0], a[1] - b[1], a[2] - b[2]};
-  const float S = sqrtf(su[0] * su[0] + su[1] * su[1] + su[2] * su[2]);
-  const float D = sqrtf(df[0] * df[0] + df[1] * df[1] + df[2] * df[2]);
-  e += 2.0f * atan2f(D, S) * wgt;
-  const float den = S * S + D * D;
+  const S h[3] = {ob[0] - ra.cx, ob[1] - ra.cy, ra.F};
+  const S hr = sqrt_(h[0] * h[0] + h[1] * h[1] + h[2] * h[2]);
+  const S hn = clamp_min(hr, kRayEps);
+  const S a[3] = {h[0] / hn, h[1] / hn, h[2] / hn};
+  const S pr = sqrt_(p0 * p0 + p1 * p1 + p2 * p2);
+  const S pn = clamp_min(pr, kRayEps);
+  const S b[3] = {p0 / pn, p1 / pn, p2 / pn};
+  const S su[3] = {a[0] + b[0], a[1] + b[1], a[2] + b[2]};
+  const S df[3] = {a[0] - b[0], a[1] - b[1], a[2] - b[2]};
+  const S Sn = sqrt_(su[0] * su[0] + su[1] * su[1] + su[2] * su[2]);
+  const S Dn = sqrt_(df[0] * df[0] + df[1] * df[1] + df[2] * df[2]);
+  e += 2.0f * atan2_(Dn, Sn) * wgt;
+  const S den = Sn * Sn + Dn * Dn;
   if constexpr (SLOPE) {
-    const float dh[3] = {-ra.dcx, -ra.dcy, ra.dF};
-    const float dp[3] = {dp0, dp1, dp2};
-    float da[3], db[3];
+    const S dh[3] = {-ra.dcx, -ra.dcy, ra.dF};
+    const S dp[3] = {dp0, dp1, dp2};
+    S da[3], db[3];
     ray_unit_backward(hr, hn, a, dh, da);  // the Jacobian of x -> x/|x| is symmetric
     ray_unit_backward(pr, pn, b, dp, db);
-    const float dS = S > 0.0f ? (su[0] * (da[0] + db[0]) + su[1] * (da[1] + db[1]) + su[2] * (da[2] + db[2])) / S : 0.0f;
-    const float dD = D > 0.0f ? (df[0] * (da[0] - db[0]) + df[1] * (da[1] - db[1]) + df[2] * (da[2] - db[2])) / D : 0.0f;
-    sl += 2.0f * wgt * (S * dD - D * dS) / den;
+    const S dS = Sn > 0.0f ? (su[0] * (da[0] + db[0]) + su[1] * (da[1] + db[1]) + su[2] * (da[2] + db[2])) / Sn : S(0.0f);
+    const S dD = Dn > 0.0f ? (df[0] * (da[0] - db[0]) + df[1] * (da[1] - db[1]) + df[2] * (da[2] - db[2])) / Dn : S(0.0f);
+    sl += 2.0f * wgt * (Sn * dD - Dn * dS) / den;
   }
   if constexpr (GRAD) {
-    const float gD = 2.0f * wgt * S / den, gS = -2.0f * wgt * D / den;  // atan2 backward
-    const float cD = D > 0.0f ? gD / D : 0.0f, cS = S > 0.0f ? gS / S : 0.0f;
-    const float ga[3] = {cS * su[0] + cD * df[0], cS * su[1] + cD * df[1], cS * su[2] + cD * df[2]};
-    const float gb[3] = {cS * su[0] - cD * df[0], cS * su[1] - cD * df[1], cS * su[2] - cD * df[2]};
-    float gh[3], gp[3];
+    const S gD = 2.0f * wgt * Sn / den, gS = -2.0f * wgt * Dn / den;  // atan2 backward
+    const S cD = Dn > 0.0f ? gD / Dn : S(0.0f), cS = Sn > 0.0f ? gS / Sn : S(0.0f);
+    const S ga[3] = {cS * su[0] + cD * df[0], cS * su[1] + cD * df[1], cS * su[2] + cD * df[2]};
+    const S gb[3] = {cS * su[0] - cD * df[0], cS * su[1] - cD * df[1], cS * su[2] - cD * df[2]};
+    S gh[3], gp[3];
     ray_unit_backward(hr, hn, a, ga, gh);
     ray_unit_backward(pr, pn, b, gb, gp);
     gin[0] += gh[2] * ra.Fp;
     gin[1] -= gh[0];
     gin[2] -= gh[1];
     G0 = gp[0]; G1 = gp[1]; G2 = gp[2];
+    go0 = gh[0]; go1 = gh[1];  // dE/d obs (u, v): h = obs - c
   }
 }
 
@@ -164,10 +174,10 @@ __device__ __forceinline__ void ray_angle_pair(const RayAngle& ra, const float* 
 //        after the first reduction without evaluating (the caller knows the answer:
 //        f(x) and phi'(0)); otherwise evaluate and return true.
 template <bool GRAD, bool SLOPE, bool TRIAL, bool DOT = false, bool CHECK = false,
-          int RES = DAVA_RESIDUAL_SQUARED_REPROJECTION>
-__device__ __forceinline__ bool ba_eval(const Layout& L, const float* x, const float* d, float alpha, const float* obs,
-                        const uint8_t* vis, float* grad, float* views, float* vpart, float* scratch, int& buf,
-                        float& E_out, float& slope_out) {
+          int RES = DAVA_RESIDUAL_SQUARED_REPROJECTION, typename S = float>
+__device__ __forceinline__ bool ba_eval(const Layout& L, const S* x, const S* d, float alpha, const float* obs,
+                                        const uint8_t* vis, S* grad, S* views, S* vpart, float* scratch, int& buf,
+                                        S& E_out, S& slope_out, S* obs_grad = nullptr) {
   static_assert(!DOT || (GRAD && !SLOPE), "DOT derives the slope from the reverse-mode gradient");
   static_assert(!CHECK || TRIAL, "CHECK needs a trial point");
   const int tid = threadIdx.x;
@@ -177,16 +187,16 @@ __device__ __forceinline__ bool ba_eval(const Layout& L, const float* x, const f
 
   // 1. per-view rotation constants (views 1..M-1), one thread per view
   for (int m = 1 + tid; m < M; m += kBlock) {
-    float* v = views + (m - 1) * kViewStride;
+    S* v = views + (m - 1) * kViewStride;
     const int r = L.rot(m), t = L.tr(m);
-    const float w0 = trial_value<TRIAL>(x, d, alpha, r + 0);
-    const float w1 = trial_value<TRIAL>(x, d, alpha, r + 1);
-    const float w2 = trial_value<TRIAL>(x, d, alpha, r + 2);
-    const float th = sqrtf(w0 * w0 + w1 * w1 + w2 * w2);
-    const float A = versine_ratio(th), B = sinc(th);
-    const float rcp = th == 0.0f ? 0.0f : 1.0f / th;
+    const S w0 = trial_value<TRIAL>(x, d, alpha, r + 0);
+    const S w1 = trial_value<TRIAL>(x, d, alpha, r + 1);
+    const S w2 = trial_value<TRIAL>(x, d, alpha, r + 2);
+    const S th = sqrt_(w0 * w0 + w1 * w1 + w2 * w2);
+    const S A = versine_ratio(th), B = sinc(th);
+    const S rcp = th == 0.0f ? S(0.0f) : 1.0f / th;
     v[VW0] = w0; v[VW1] = w1; v[VW2] = w2;
-    v[VCOS] = cosf(th); v[VA] = A; v[VB] = B; v[VSIN] = sinf(th);
+    v[VCOS] = cos_(th); v[VA] = A; v[VB] = B; v[VSIN] = sin_(th);
     v[VRCP] = rcp;
     v[VAP] = rcp * (B - 2.0f * A);       // d/dth (1-cos)/th^2, reference backward form
     v[VTC] = th * sinc_slope(th);        // d/dth sin(th)/th
@@ -194,7 +204,7 @@ __device__ __forceinline__ bool ba_eval(const Layout& L, const float* x, const f
     v[VT1] = trial_value<TRIAL>(x, d, alpha, t + 1);
     v[VT2] = trial_value<TRIAL>(x, d, alpha, t + 2);
     if constexpr (SLOPE) {
-      const float d0 = d[r], d1 = d[r + 1], d2 = d[r + 2];
+      const S d0 = d[r], d1 = d[r + 1], d2 = d[r + 2];
       v[VDW0] = d0; v[VDW1] = d1; v[VDW2] = d2;
       v[VDTH] = (w0 * d0 + w1 * d1 + w2 * d2) * rcp;
       v[VDT0] = d[t]; v[VDT1] = d[t + 1]; v[VDT2] = d[t + 2];
@@ -202,13 +212,13 @@ __device__ __forceinline__ bool ba_eval(const Layout& L, const float* x, const f
   }
 
   // 2. scale normalisation s = (mean|X| N + mean|t| M)/(N+M), and its slope
-  float sums[3] = {0.f, 0.f, 0.f};  // sum|X|, sum sgn(X) dX (SLOPE or DOT), moved (CHECK)
+  S sums[3] = {0.f, 0.f, 0.f};  // sum|X|, sum sgn(X) dX (SLOPE or DOT), moved (CHECK)
   bool moved = false;
   for (int n = tid; n < N; n += kBlock) {
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
-      const float X = trial_value<TRIAL>(x, d, alpha, L.pt(n) + c);
-      sums[0] += fabsf(X);
+      const S X = trial_value<TRIAL>(x, d, alpha, L.pt(n) + c);
+      sums[0] += fabs_(X);
       if constexpr (SLOPE || DOT) sums[1] += sgn(X) * d[L.pt(n) + c];
       if constexpr (CHECK) moved |= X != x[L.pt(n) + c];
     }
@@ -223,38 +233,38 @@ __device__ __forceinline__ bool ba_eval(const Layout& L, const float* x, const f
     sums[2] = moved ? 1.f : 0.f;
     block_sum<3>(sums, scratch, buf);
   } else if constexpr (SLOPE || DOT) {
-    block_sum<2>(reinterpret_cast<float(&)[2]>(sums), scratch, buf);
+    block_sum<2>(reinterpret_cast<S(&)[2]>(sums), scratch, buf);
   } else {
-    block_sum<1>(reinterpret_cast<float(&)[1]>(sums), scratch, buf);
+    block_sum<1>(reinterpret_cast<S(&)[1]>(sums), scratch, buf);
   }
   buf ^= 1;  // (this barrier also publishes the view constants)
   if constexpr (CHECK) {
     if (sums[2] == 0.f) return false;  // uniform: every thread holds the same sums
   }
-  float tsum = 0.f, tdsum = 0.f;
+  S tsum = 0.f, tdsum = 0.f;
   for (int i = L.tr(1); i < L.tr(1) + 3 * (M - 1); ++i) {
-    const float t = trial_value<TRIAL>(x, d, alpha, i);
-    tsum += fabsf(t);
+    const S t = trial_value<TRIAL>(x, d, alpha, i);
+    tsum += fabs_(t);
     if constexpr (SLOPE) tdsum += sgn(t) * d[i];
   }
   const float fN = (float)N, fM = (float)M, fNM = (float)(N + M);
-  const float ps = sums[0] / (3.0f * fN);
-  const float cs = tsum / (3.0f * (float)(M - 1));
-  const float s = (ps * fN + cs * fM) / fNM;
-  const float inv_s = 1.0f / s;
-  float ds_over_s = 0.f;
+  const S ps = sums[0] / (3.0f * fN);
+  const S cs = tsum / (3.0f * (float)(M - 1));
+  const S s = (ps * fN + cs * fM) / fNM;
+  const S inv_s = 1.0f / s;
+  S ds_over_s = 0.f;
   if constexpr (SLOPE) {
-    const float ds = ((sums[1] / (3.0f * fN)) * fN + (tdsum / (3.0f * (float)(M - 1))) * fM) / fNM;
+    const S ds = ((sums[1] / (3.0f * fN)) * fN + (tdsum / (3.0f * (float)(M - 1))) * fM) / fNM;
     ds_over_s = ds * inv_s;
   }
 
   // 3. intrinsics (trial values + directions)
-  Intrinsics in, din;
+  Intrinsics<S> in, din;
   in.f = trial_value<TRIAL>(x, d, alpha, 0);
   in.cx = trial_value<TRIAL>(x, d, alpha, 1);
   in.cy = trial_value<TRIAL>(x, d, alpha, 2);
   in.k1 = in.k2 = in.k3 = in.p1 = in.p2 = 0.f;
-  din = Intrinsics{0, 0, 0, 0, 0, 0, 0, 0};
+  din = Intrinsics<S>{0, 0, 0, 0, 0, 0, 0, 0};
   const int kd = L.dist();
   if (L.distort) {
     in.k1 = trial_value<TRIAL>(x, d, alpha, kd + 0);
@@ -268,26 +278,26 @@ __device__ __forceinline__ bool ba_eval(const Layout& L, const float* x, const f
     if (L.distort) { din.k1 = d[kd]; din.k2 = d[kd + 1]; din.k3 = d[kd + 2]; din.p1 = d[kd + 3]; din.p2 = d[kd + 4]; }
   }
 
-  RayAngle ra{};
+  RayAngle<S> ra{};
   if constexpr (RES == DAVA_RESIDUAL_RAY_ANGLE) {
     ra.cx = in.cx;
     ra.cy = in.cy;
-    ra.F = (in.f > 0.0f ? in.f : expm1f(in.f)) + 1.0f;  // elu(f) + 1
-    ra.Fp = in.f > 0.0f ? 1.0f : expf(in.f);
+    ra.F = (in.f > 0.0f ? in.f : expm1_(in.f)) + 1.0f;  // elu(f) + 1
+    ra.Fp = in.f > 0.0f ? 1.0f : exp_(in.f);
     if constexpr (SLOPE) { ra.dcx = din.cx; ra.dcy = din.cy; ra.dF = ra.Fp * din.f; }
   }
 
-  float e_loc = 0.f, sl_loc = 0.f;
-  float gin[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // f cx cy k1 k2 k3 p1 p2
-  float gsx = 0.f;                          // sum gX~ . X  (scale path)
-  float gdx = 0.f;                          // DOT: sum gX~ . dX
+  S e_loc = 0.f, sl_loc = 0.f;
+  S gin[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // f cx cy k1 k2 k3 p1 p2
+  S gsx = 0.f;                          // sum gX~ . X  (scale path)
+  S gdx = 0.f;                          // DOT: sum gX~ . dX
 
   // 4. sweep views (outer) x own points (inner)
   for (int m = 0; m < M; ++m) {
-    const float* v = views + (m > 0 ? (m - 1) * kViewStride : 0);
-    float vc = 1.f, vA = 0.f, vB = 0.f, vs = 0.f, vAp = 0.f, vTC = 0.f;
-    float w0 = 0.f, w1 = 0.f, w2 = 0.f, tt0 = 0.f, tt1 = 0.f, tt2 = 0.f;
-    float dw0 = 0.f, dw1 = 0.f, dw2 = 0.f, dth = 0.f, dtt0 = 0.f, dtt1 = 0.f, dtt2 = 0.f;
+    const S* v = views + (m > 0 ? (m - 1) * kViewStride : 0);
+    S vc = 1.f, vA = 0.f, vB = 0.f, vs = 0.f, vAp = 0.f, vTC = 0.f;
+    S w0 = 0.f, w1 = 0.f, w2 = 0.f, tt0 = 0.f, tt1 = 0.f, tt2 = 0.f;
+    S dw0 = 0.f, dw1 = 0.f, dw2 = 0.f, dth = 0.f, dtt0 = 0.f, dtt1 = 0.f, dtt2 = 0.f;
     if (m > 0) {
       w0 = v[VW0]; w1 = v[VW1]; w2 = v[VW2];
       vc = v[VCOS]; vA = v[VA]; vB = v[VB]; vs = v[VSIN]; vAp = v[VAP]; vTC = v[VTC];
@@ -299,23 +309,23 @@ __device__ __forceinline__ bool ba_eval(const Layout& L, const float* x, const f
         dtt2 = (v[VDT2] - tt2 * (ds_over_s * s)) * inv_s;
       }
     }
-    float vg[7] = {0, 0, 0, 0, 0, 0, 0};  // gw_direct xyz, g_theta, g_t~ xyz
+    S vg[7] = {0, 0, 0, 0, 0, 0, 0};  // gw_direct xyz, g_theta, g_t~ xyz
 
     for (int n = tid; n < N; n += kBlock) {
       const int ip = L.pt(n);
-      const float X0 = trial_value<TRIAL>(x, d, alpha, ip + 0);
-      const float X1 = trial_value<TRIAL>(x, d, alpha, ip + 1);
-      const float X2 = trial_value<TRIAL>(x, d, alpha, ip + 2);
-      const float a0 = X0 * inv_s, a1 = X1 * inv_s, a2 = X2 * inv_s;  // X~ = X / s
-      float da0 = 0.f, da1 = 0.f, da2 = 0.f;
+      const S X0 = trial_value<TRIAL>(x, d, alpha, ip + 0);
+      const S X1 = trial_value<TRIAL>(x, d, alpha, ip + 1);
+      const S X2 = trial_value<TRIAL>(x, d, alpha, ip + 2);
+      const S a0 = X0 * inv_s, a1 = X1 * inv_s, a2 = X2 * inv_s;  // X~ = X / s
+      S da0 = 0.f, da1 = 0.f, da2 = 0.f;
       if constexpr (SLOPE) {
         da0 = (d[ip + 0] - a0 * (ds_over_s * s)) * inv_s;
         da1 = (d[ip + 1] - a1 * (ds_over_s * s)) * inv_s;
         da2 = (d[ip + 2] - a2 * (ds_over_s * s)) * inv_s;
       }
       // camera-relative point p (and dp)
-      float p0, p1, p2, dp0 = 0.f, dp1 = 0.f, dp2 = 0.f;
-      float vw = 0.f, c0 = 0.f, c1 = 0.f, c2 = 0.f;  // v.w and w x v
+      S p0, p1, p2, dp0 = 0.f, dp1 = 0.f, dp2 = 0.f;
+      S vw = 0.f, c0 = 0.f, c1 = 0.f, c2 = 0.f;  // v.w and w x v
       if (m == 0) {
         p0 = a0; p1 = a1; p2 = a2;
         if constexpr (SLOPE) { dp0 = da0; dp1 = da1; dp2 = da2; }
@@ -324,40 +334,41 @@ __device__ __forceinline__ bool ba_eval(const Layout& L, const float* x, const f
         c0 = w1 * a2 - w2 * a1;
         c1 = w2 * a0 - w0 * a2;
         c2 = w0 * a1 - w1 * a0;
-        const float Avw = vA * vw;
+        const S Avw = vA * vw;
         p0 = a0 * vc + Avw * w0 + c0 * vB + tt0;
         p1 = a1 * vc + Avw * w1 + c1 * vB + tt1;
         p2 = a2 * vc + Avw * w2 + c2 * vB + tt2;
         if constexpr (SLOPE) {
-          const float dc = -vs * dth, dA = vAp * dth, dB = vTC * dth;
-          const float dvw = (da0 * w0 + da1 * w1 + da2 * w2) + (a0 * dw0 + a1 * dw1 + a2 * dw2);
-          const float e0 = (dw1 * a2 - dw2 * a1) + (w1 * da2 - w2 * da1);
-          const float e1 = (dw2 * a0 - dw0 * a2) + (w2 * da0 - w0 * da2);
-          const float e2 = (dw0 * a1 - dw1 * a0) + (w0 * da1 - w1 * da0);
-          const float k = dA * vw + vA * dvw;
+          const S dc = -vs * dth, dA = vAp * dth, dB = vTC * dth;
+          const S dvw = (da0 * w0 + da1 * w1 + da2 * w2) + (a0 * dw0 + a1 * dw1 + a2 * dw2);
+          const S e0 = (dw1 * a2 - dw2 * a1) + (w1 * da2 - w2 * da1);
+          const S e1 = (dw2 * a0 - dw0 * a2) + (w2 * da0 - w0 * da2);
+          const S e2 = (dw0 * a1 - dw1 * a0) + (w0 * da1 - w1 * da0);
+          const S k = dA * vw + vA * dvw;
           dp0 = da0 * vc + a0 * dc + k * w0 + Avw * dw0 + e0 * vB + c0 * dB + dtt0;
           dp1 = da1 * vc + a1 * dc + k * w1 + Avw * dw1 + e1 * vB + c1 * dB + dtt1;
           dp2 = da2 * vc + a2 * dc + k * w2 + Avw * dw2 + e2 * vB + c2 * dB + dtt2;
         }
       }
-      float G0 = 0.f, G1 = 0.f, G2 = 0.f;  // dE/dp
+      S G0 = 0.f, G1 = 0.f, G2 = 0.f;  // dE/dp
+      S go0 = 0.f, go1 = 0.f;          // dE/d obs (second-order instantiations only)
       if constexpr (RES == DAVA_RESIDUAL_SQUARED_REPROJECTION) {
         // projection
-        const float iz = 1.0f / p2;
-        const float qx = p0 * iz, qy = p1 * iz;
-        const float ub = in.f * qx, vb = in.f * qy;
-        float u, vv, dub = 0.f, dvb = 0.f;
-        float Juu = 1.f, Juv = 0.f, Jvv = 1.f, r2 = 0.f;
+        const S iz = 1.0f / p2;
+        const S qx = p0 * iz, qy = p1 * iz;
+        const S ub = in.f * qx, vb = in.f * qy;
+        S u, vv, dub = 0.f, dvb = 0.f;
+        S Juu = 1.f, Juv = 0.f, Jvv = 1.f, r2 = 0.f;
         if constexpr (SLOPE) {
-          const float dqx = (dp0 - qx * dp2) * iz, dqy = (dp1 - qy * dp2) * iz;
+          const S dqx = (dp0 - qx * dp2) * iz, dqy = (dp1 - qy * dp2) * iz;
           dub = din.f * qx + in.f * dqx;
           dvb = din.f * qy + in.f * dqy;
         }
         if (L.distort) {
           r2 = ub * ub + vb * vb;
-          const float D = 1.0f + in.k1 * r2 + in.k2 * r2 * r2 + in.k3 * r2 * r2 * r2;
-          const float Dr = in.k1 + 2.0f * in.k2 * r2 + 3.0f * in.k3 * r2 * r2;
-          const float uvb = ub * vb;
+          const S D = 1.0f + in.k1 * r2 + in.k2 * r2 * r2 + in.k3 * r2 * r2 * r2;
+          const S Dr = in.k1 + 2.0f * in.k2 * r2 + 3.0f * in.k3 * r2 * r2;
+          const S uvb = ub * vb;
           u = ub * D + 2.0f * in.p1 * uvb + in.p2 * (r2 + 2.0f * ub * ub) + in.cx;
           vv = vb * D + 2.0f * in.p2 * uvb + in.p1 * (r2 + 2.0f * vb * vb) + in.cy;
           Juu = D + 2.0f * ub * ub * Dr + 2.0f * in.p1 * vb + 6.0f * in.p2 * ub;
@@ -369,13 +380,13 @@ __device__ __forceinline__ bool ba_eval(const Layout& L, const float* x, const f
         }
         const int pair = m * N + n;
         const float wgt = vis[pair] ? 1.0f : 0.0f;
-        const float ru = u - obs[2 * pair], rv = vv - obs[2 * pair + 1];
+        const S ru = u - obs[2 * pair], rv = vv - obs[2 * pair + 1];
         e_loc += (ru * ru + rv * rv) * wgt;
         if constexpr (SLOPE) {
-          float du = Juu * dub + Juv * dvb + din.cx;
-          float dv = Juv * dub + Jvv * dvb + din.cy;
+          S du = Juu * dub + Juv * dvb + din.cx;
+          S dv = Juv * dub + Jvv * dvb + din.cy;
           if (L.distort) {
-            const float r4 = r2 * r2;
+            const S r4 = r2 * r2;
             du += ub * (r2 * din.k1 + r4 * din.k2 + r4 * r2 * din.k3) + 2.0f * ub * vb * din.p1 +
                   (r2 + 2.0f * ub * ub) * din.p2;
             dv += vb * (r2 * din.k1 + r4 * din.k2 + r4 * r2 * din.k3) + (r2 + 2.0f * vb * vb) * din.p1 +
@@ -384,15 +395,17 @@ __device__ __forceinline__ bool ba_eval(const Layout& L, const float* x, const f
           sl_loc += 2.0f * wgt * (ru * du + rv * dv);
         }
         if constexpr (GRAD) {
-          const float gu = 2.0f * wgt * ru, gv = 2.0f * wgt * rv;
+          const S gu = 2.0f * wgt * ru, gv = 2.0f * wgt * rv;
+          go0 = -gu;
+          go1 = -gv;
           gin[1] += gu;
           gin[2] += gv;
-          float gub = gu, gvb = gv;
+          S gub = gu, gvb = gv;
           if (L.distort) {
             gub = gu * Juu + gv * Juv;
             gvb = gu * Juv + gv * Jvv;
-            const float r4 = r2 * r2;
-            const float gr = gu * ub + gv * vb;
+            const S r4 = r2 * r2;
+            const S gr = gu * ub + gv * vb;
             gin[3] += gr * r2;
             gin[4] += gr * r4;
             gin[5] += gr * r4 * r2;
@@ -400,22 +413,29 @@ __device__ __forceinline__ bool ba_eval(const Layout& L, const float* x, const f
             gin[7] += gu * (r2 + 2.0f * ub * ub) + gv * 2.0f * ub * vb;
           }
           gin[0] += gub * qx + gvb * qy;
-          const float fi = in.f * iz;
+          const S fi = in.f * iz;
           G0 = gub * fi; G1 = gvb * fi; G2 = -(gub * ub + gvb * vb) * iz;
         }
       } else {
-        ray_angle_pair<GRAD, SLOPE>(ra, obs + 2 * (m * N + n), vis[m * N + n], p0, p1, p2, dp0, dp1, dp2,
-                                    e_loc, sl_loc, gin, G0, G1, G2);
+        ray_angle_pair<GRAD, SLOPE, S>(ra, obs + 2 * (m * N + n), vis[m * N + n], p0, p1, p2, dp0, dp1, dp2,
+                                    e_loc, sl_loc, gin, G0, G1, G2, go0, go1);
+      }
+      if constexpr (GRAD && !std::is_same<S, float>::value) {
+        if (obs_grad) {
+          const int pr = m * N + n;
+          obs_grad[2 * pr] = go0;
+          obs_grad[2 * pr + 1] = go1;
+        }
       }
       if constexpr (GRAD) {
-        float gx0, gx1, gx2;
+        S gx0, gx1, gx2;
         if (m == 0) {
           gx0 = G0; gx1 = G1; gx2 = G2;
         } else {
-          const float Gw = G0 * w0 + G1 * w1 + G2 * w2;
-          const float Gv = G0 * a0 + G1 * a1 + G2 * a2;
-          const float Gx = G0 * c0 + G1 * c1 + G2 * c2;
-          const float AGw = vA * Gw, Avw = vA * vw;
+          const S Gw = G0 * w0 + G1 * w1 + G2 * w2;
+          const S Gv = G0 * a0 + G1 * a1 + G2 * a2;
+          const S Gx = G0 * c0 + G1 * c1 + G2 * c2;
+          const S AGw = vA * Gw, Avw = vA * vw;
           // dE/dX~ = c G + A (G.w) w + B (G x w)
           gx0 = vc * G0 + AGw * w0 + vB * (G1 * w2 - G2 * w1);
           gx1 = vc * G1 + AGw * w1 + vB * (G2 * w0 - G0 * w2);
@@ -427,7 +447,7 @@ __device__ __forceinline__ bool ba_eval(const Layout& L, const float* x, const f
           vg[3] += -vs * Gv + vAp * vw * Gw + vTC * Gx;  // dE/dth
           vg[4] += G0; vg[5] += G1; vg[6] += G2;          // dE/dt~
         }
-        float* gp = grad + ip;
+        S* gp = grad + ip;
         if (m == 0) { gp[0] = gx0; gp[1] = gx1; gp[2] = gx2; }
         else { gp[0] += gx0; gp[1] += gx1; gp[2] += gx2; }
         if (m == M - 1) {
@@ -440,7 +460,7 @@ __device__ __forceinline__ bool ba_eval(const Layout& L, const float* x, const f
       if (m > 0) {
 #pragma unroll
         for (int k = 0; k < 7; ++k) {
-          const float w = wave_sum(vg[k]);
+          const S w = wave_sum(vg[k]);
           if (lane == 0) vpart[(m * kWaves + wave) * kViewPart + k] = w;
         }
       }
@@ -449,44 +469,44 @@ __device__ __forceinline__ bool ba_eval(const Layout& L, const float* x, const f
 
   // 5. block reduction of error, slope, intrinsics gradient and scale-path sum
   if constexpr (GRAD) {
-    float r[12] = {e_loc, sl_loc, gin[0], gin[1], gin[2], gin[3], gin[4], gin[5], gin[6], gin[7], gsx, gdx};
+    S r[12] = {e_loc, sl_loc, gin[0], gin[1], gin[2], gin[3], gin[4], gin[5], gin[6], gin[7], gsx, gdx};
     if constexpr (DOT) block_sum<12>(r, scratch, buf);
-    else block_sum<11>(reinterpret_cast<float(&)[11]>(r), scratch, buf);
+    else block_sum<11>(reinterpret_cast<S(&)[11]>(r), scratch, buf);
     buf ^= 1;
     E_out = r[0];
     slope_out = r[1];
     // scale path: s = (ps N + cs M)/(N+M); X~ = X/s, t~ = t/s
-    float gst = 0.f;  // sum g_t~ . t
+    S gst = 0.f;  // sum g_t~ . t
     for (int m = 1; m < M; ++m) {
-      const float* v = views + (m - 1) * kViewStride;
+      const S* v = views + (m - 1) * kViewStride;
 #pragma unroll
       for (int c = 0; c < 3; ++c) {
-        const float* q = vpart + (m * kWaves) * kViewPart + 4 + c;
-        const float g = ((q[0] + q[kViewPart]) + q[2 * kViewPart]) + q[3 * kViewPart];
+        const S* q = vpart + (m * kWaves) * kViewPart + 4 + c;
+        const S g = ((q[0] + q[kViewPart]) + q[2 * kViewPart]) + q[3 * kViewPart];
         gst += g * v[VT0 + c];
       }
     }
-    const float gs = -(r[10] + gst) * inv_s * inv_s;
-    const float g_ps = gs * fN / fNM, g_cs = gs * fM / fNM;
-    const float gabsX = g_ps / (3.0f * fN);
-    const float gabsT = g_cs / (3.0f * (float)(M - 1));
+    const S gs = -(r[10] + gst) * inv_s * inv_s;
+    const S g_ps = gs * fN / fNM, g_cs = gs * fM / fNM;
+    const S gabsX = g_ps / (3.0f * fN);
+    const S gabsT = g_cs / (3.0f * (float)(M - 1));
     if constexpr (DOT) {
       // d . grad = (1/s) sum d.gX~ + gabsX sum d.sgn(X) + views + intrinsics (all threads, same order)
-      float dv = 0.f;
+      S dv = 0.f;
       for (int m = 1; m < M; ++m) {
-        const float* v = views + (m - 1) * kViewStride;
+        const S* v = views + (m - 1) * kViewStride;
         auto vs = [&](int k) {
-          const float* p = vpart + (m * kWaves) * kViewPart + k;
+          const S* p = vpart + (m * kWaves) * kViewPart + k;
           return ((p[0] + p[kViewPart]) + p[2 * kViewPart]) + p[3 * kViewPart];
         };
-        const float gth = vs(3) * v[VRCP];
+        const S gth = vs(3) * v[VRCP];
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
           dv += d[L.tr(m) + c] * (vs(4 + c) * inv_s + sgn(v[VT0 + c]) * gabsT);
           dv += d[L.rot(m) + c] * (vs(c) + gth * v[VW0 + c]);
         }
       }
-      float di = d[0] * r[2] + d[1] * r[3] + d[2] * r[4];
+      S di = d[0] * r[2] + d[1] * r[3] + d[2] * r[4];
       if (L.distort) {
 #pragma unroll
         for (int k = 0; k < 5; ++k) di += d[kd + k] * r[5 + k];
@@ -494,18 +514,18 @@ __device__ __forceinline__ bool ba_eval(const Layout& L, const float* x, const f
       slope_out = (r[11] * inv_s + gabsX * sums[1]) + dv + di;
     }
     for (int n = tid; n < N; n += kBlock) {
-      float* gp = grad + L.pt(n);
+      S* gp = grad + L.pt(n);
 #pragma unroll
       for (int c = 0; c < 3; ++c) {
-        const float X = trial_value<TRIAL>(x, d, alpha, L.pt(n) + c);
+        const S X = trial_value<TRIAL>(x, d, alpha, L.pt(n) + c);
         gp[c] = gp[c] * inv_s + sgn(X) * gabsX;
       }
     }
     for (int q = tid; q < 6 * (M - 1); q += kBlock) {
       const int m = 1 + q / 6, c = q % 6;
-      const float* v = views + (m - 1) * kViewStride;
+      const S* v = views + (m - 1) * kViewStride;
       auto vsum = [&](int k) {
-        const float* p = vpart + (m * kWaves) * kViewPart + k;
+        const S* p = vpart + (m * kWaves) * kViewPart + k;
         return ((p[0] + p[kViewPart]) + p[2 * kViewPart]) + p[3 * kViewPart];
       };
       if (c < 3) {
@@ -524,9 +544,9 @@ __device__ __forceinline__ bool ba_eval(const Layout& L, const float* x, const f
     }
     __syncthreads();
   } else {
-    float r[2] = {e_loc, sl_loc};
+    S r[2] = {e_loc, sl_loc};
     if constexpr (SLOPE) block_sum<2>(r, scratch, buf);
-    else block_sum<1>(reinterpret_cast<float(&)[1]>(r), scratch, buf);
+    else block_sum<1>(reinterpret_cast<S(&)[1]>(r), scratch, buf);
     buf ^= 1;
     E_out = r[0];
     slope_out = r[1];

@@ -467,7 +467,7 @@ __global__ __launch_bounds__(kBlock, DAVA_SOLVE_WAVES_PER_EU) void bfgs_ba_solve
     if (have_next) {
       E = E_next;
     } else {
-      ba_eval<true, false, false, false, false, RES>(L, x, nullptr, 0.f, obs, vis, g, views, vpart, scratch, buf, E,
+      ba_eval<true, false, false, false, false, RES, float>(L, x, nullptr, 0.f, obs, vis, g, views, vpart, scratch, buf, E,
                                                      unused);
       ++evals;
     }
@@ -576,7 +576,7 @@ __global__ __launch_bounds__(kBlock, DAVA_SOLVE_WAVES_PER_EU) void bfgs_ba_solve
       // phi'(0).  The check rides on the objective's first reduction (CHECK).  Otherwise
       // E and the full gradient at the trial point are formed (kept for reuse as the
       // next iterate's gradient) and phi'(alpha) = d . grad (DOT).
-      if (ba_eval<true, !DAVA_TRIAL_DOT, true, DAVA_TRIAL_DOT, DAVA_TRIAL_CHECK, RES>(L, x, d, al, obs, vis, gp, views, vpart,
+      if (ba_eval<true, !DAVA_TRIAL_DOT, true, DAVA_TRIAL_DOT, DAVA_TRIAL_CHECK, RES, float>(L, x, d, al, obs, vis, gp, views, vpart,
                                                                      scratch, buf, fa, dfa)) {
         ++evals;
         last_same = false;
@@ -642,7 +642,7 @@ __global__ __launch_bounds__(kBlock, DAVA_SOLVE_WAVES_PER_EU) void bfgs_ba_solve
   for (int i = tid; i < P; i += kBlock) xo[i] = x[i];
   if (a.err_out) {
     float e2 = 0.f;
-    ba_eval<false, false, false, false, false, RES>(L, x, nullptr, 0.f, obs, vis, nullptr, views, vpart, scratch, buf,
+    ba_eval<false, false, false, false, false, RES, float>(L, x, nullptr, 0.f, obs, vis, nullptr, views, vpart, scratch, buf,
                                                    e2, unused);
     if (tid == 0) a.err_out[b] = e2;
   }
@@ -707,7 +707,7 @@ __global__ __launch_bounds__(kBlock) void ba_evaluate_kernel(EvalArgs a) {
   const float al = (TRIAL && a.alpha) ? a.alpha[b] : 0.f;
   int buf = 0;
   float E = 0.f, sl = 0.f;
-  ba_eval<GRAD, SLOPE, TRIAL, false, false, RES>(L, x, d, al, obs, vis, g, views, vpart, scratch, buf, E, sl);
+  ba_eval<GRAD, SLOPE, TRIAL, false, false, RES, float>(L, x, d, al, obs, vis, g, views, vpart, scratch, buf, E, sl);
   if (tid == 0) {
     a.err[b] = E;
     if (SLOPE && a.slope) a.slope[b] = sl;

@@ -61,6 +61,7 @@ SIGNATURES = {
     "dava_ba_solve": (ctypes.c_int, [ctypes.POINTER(DavaScene), ctypes.POINTER(DavaSolverConfig), _vp, _vp, _vp, _vp,
                                      _vp, ctypes.c_size_t, _vp]),
     "dava_ba_evaluate": (ctypes.c_int, [ctypes.POINTER(DavaScene), _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "dava_ba_second_order": (ctypes.c_int, [ctypes.POINTER(DavaScene)] + [_vp] * 8),
     "dava_abi_version": (ctypes.c_int, []),
     "dava_status_string": (ctypes.c_char_p, [ctypes.c_int]),
     "dava_device_arch": (ctypes.c_char_p, []),

@@ -19,12 +19,12 @@ Differentiating through the solve (``parameters.requires_grad``, the reference's
 graph kept: the closure's gradient is taken with ``create_graph=True`` by
 PyTorch, and every solver op (initial scale, rescale, update, search direction)
 is an autograd node whose backward is a HIP kernel (csrc/bfgs_grad.hip); the
-line search is detached, as in the reference.  The fused objectives
-(:class:`ReprojectionError`, :class:`RayAngleError`) provide first derivatives
-only, so in that mode they must be replaced by a differentiable closure.
+line search is detached, as in the reference.  A fused objective
+(:class:`ReprojectionError`, :class:`RayAngleError`) then acts as a closure whose
+double backward is the forward-over-reverse kernel (H v and the observation
+cross term, csrc/ba_second_order.hip), so gradients reach captured observations.
 
-Not supported (raises rather than silently falling back): CPU tensors, and
-second derivatives of the fused objectives.
+Not supported (raises rather than silently falling back): CPU tensors.
 """
 from typing import Callable, Optional
 
@@ -84,11 +84,6 @@ class BFGSSolver(Module):
     def forward(self, parameters: torch.Tensor,
                 error_function: Callable[[torch.Tensor, torch.Tensor], torch.Tensor]) -> torch.Tensor:
         _native.require_device_tensor(parameters, "parameters")
-        if parameters.requires_grad and isinstance(error_function, ReprojectionError):
-            raise NotImplementedError(
-                "differentiating through the solve needs second derivatives of the error function; the fused "
-                "ReprojectionError / RayAngleError kernels provide first derivatives only -- pass a "
-                "differentiable closure (e.g. the reference's torch error_function) or detach the initial guess")
         if self.training:
             error_threshold, num_iterations = self.training_error_threshold, self.training_iterations
         else:

@@ -6,8 +6,9 @@ same shapes, same ValueError on a wrong P).  ``ReprojectionError`` is the
 error-function object the drop-in ``BFGSSolver`` recognises and runs fully
 fused on the GPU; it is also an ordinary ``error_function(parameters,
 batch_mask)`` closure (``networks/calibration_network.py:58-67`` contract)
-whose value and first derivative come from the HIP objective kernel, so it
-works with any caller that only needs first-order autograd.
+whose value and derivatives (first order, and second order for
+create_graph callers: H v and the observation cross term) come from HIP
+kernels, differentiable w.r.t. the parameters and the observations.
 """
 from typing import NamedTuple
 
@@ -46,20 +47,66 @@ def unpack_calibration_parameters(parameters: torch.Tensor, num_views: int, num_
 
 
 class _NativeObjective(torch.autograd.Function):
-    """E(x) per row with dE/dx from the HIP reverse-mode kernel (first order only)."""
+    """E(x, obs) per row from the HIP objective kernel.  Its backward is itself
+    differentiable (``_NativeGradient``), so ``torch.autograd.grad(..., create_graph=True)``
+    -- the reference's differentiate-through-the-solve mode -- gets exact second
+    derivatives from the forward-over-reverse kernel (``dava_ba_second_order``)."""
 
     @staticmethod
     def forward(ctx, x, observations, visibility, num_views, num_points, distortion, residual):
-        err, grad, _ = native_ops.ba_evaluate(x, observations, visibility, num_views, num_points, distortion,
-                                              want_grad=ctx.needs_input_grad[0], residual=residual)
-        ctx.save_for_backward(grad if grad is not None else err)
+        need_x, need_obs = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
+        if need_obs:  # dE/dobs comes from the second-order kernel (v = 0)
+            err, grad, _, obs_grad, _ = native_ops.ba_second_order(
+                x, observations, visibility, num_views, num_points, distortion, residual=residual, want_hv=False)
+        else:
+            err, grad, _ = native_ops.ba_evaluate(x, observations, visibility, num_views, num_points, distortion,
+                                                  want_grad=need_x, residual=residual)
+            obs_grad = None
+        ctx.save_for_backward(x, observations, visibility)
+        ctx.meta = (num_views, num_points, distortion, residual)
+        ctx.first = (grad, obs_grad)
         return err
 
     @staticmethod
-    @torch.autograd.function.once_differentiable
     def backward(ctx, grad_out):
-        (grad,) = ctx.saved_tensors
-        return grad_out.unsqueeze(-1) * grad, None, None, None, None, None, None
+        x, obs, vis = ctx.saved_tensors
+        need_x, need_obs = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
+        if torch.is_grad_enabled():  # create_graph: keep the gradient differentiable
+            grad, obs_grad = _NativeGradient.apply(x, obs, vis, *ctx.meta)
+        else:
+            grad, obs_grad = ctx.first
+        gx = grad_out.unsqueeze(-1) * grad if need_x else None
+        gobs = grad_out[:, None, None, None] * obs_grad if (need_obs and obs_grad is not None) else None
+        return gx, gobs, None, None, None, None, None
+
+
+class _NativeGradient(torch.autograd.Function):
+    """(dE/dx, dE/dobs) as a differentiable function of (x, obs): its VJP along the x-cotangent
+    u is (H u, (d2E/dobs dx) u), from one forward-over-reverse launch."""
+
+    @staticmethod
+    def forward(ctx, x, observations, visibility, num_views, num_points, distortion, residual):
+        _, grad, _, obs_grad, _ = native_ops.ba_second_order(
+            x, observations, visibility, num_views, num_points, distortion, residual=residual, want_hv=False)
+        ctx.save_for_backward(x, observations, visibility)
+        ctx.meta = (num_views, num_points, distortion, residual)
+        ctx.set_materialize_grads(False)
+        return grad, obs_grad
+
+    @staticmethod
+    @torch.autograd.function.once_differentiable
+    def backward(ctx, u, u_obs):
+        if u_obs is not None and bool((u_obs != 0).any()):
+            raise NotImplementedError("differentiating dE/dobs again (second derivatives in the observations) "
+                                      "is not implemented for the fused objectives")
+        if u is None:
+            return None, None, None, None, None, None, None
+        x, obs, vis = ctx.saved_tensors
+        _, _, hv, _, obs_hv = native_ops.ba_second_order(x, obs, vis, *ctx.meta[:3], direction=u,
+                                                          residual=ctx.meta[3],
+                                                          want_obs=ctx.needs_input_grad[1])
+        return (hv if ctx.needs_input_grad[0] else None, obs_hv if ctx.needs_input_grad[1] else None,
+                None, None, None, None, None)
 
 
 class ReprojectionError:

@@ -55,6 +55,33 @@ def ba_evaluate(x: torch.Tensor, observations: torch.Tensor, visibility: torch.T
     return err, grad, slope
 
 
+def ba_second_order(x: torch.Tensor, observations: torch.Tensor, visibility: torch.Tensor, num_views: int,
+                    num_points: int, distortion: bool = False, direction: Optional[torch.Tensor] = None,
+                    residual: int = N.DAVA_RESIDUAL_SQUARED_REPROJECTION, want_hv: bool = True,
+                    want_obs: bool = True):
+    """(E, dE/dx, H v, dE/dobs, (d2E/dobs dx) v) for a (B, P) fp32 batch (``dava_ba_second_order``).
+    ``direction`` None means v = 0 (then only E, dE/dx and dE/dobs are meaningful)."""
+    lib = N.load_library()
+    N.require_device_tensor(x, "x")
+    if x.dtype != torch.float32:
+        raise TypeError("the fused BA kernels compute in float32 (the reference's BA dtype)")
+    x = _c(x.detach())
+    b = x.shape[0]
+    obs = _c(observations.detach().to(torch.float32))
+    vis = _c(visibility.detach().to(torch.uint8))
+    v = _c(direction.detach().to(torch.float32)) if direction is not None else None
+    err = torch.empty(b, device=x.device, dtype=torch.float32)
+    grad = torch.empty_like(x)
+    hv = torch.empty_like(x) if want_hv else None
+    obs_grad = torch.empty_like(obs) if want_obs else None
+    obs_hv = torch.empty_like(obs) if (want_obs and want_hv) else None
+    sc = scene_struct(obs, vis, num_views, num_points, distortion, b, residual)
+    with torch.cuda.device(x.device):
+        N.check(lib.dava_ba_second_order(sc, N.ptr(x), N.ptr(v), N.ptr(err), N.ptr(grad), N.ptr(hv), N.ptr(obs_grad),
+                                         N.ptr(obs_hv), N.stream_of(x.device)), "dava_ba_second_order")
+    return err, grad, hv, obs_grad, obs_hv
+
+
 def ba_solve(x0: torch.Tensor, observations: torch.Tensor, visibility: torch.Tensor, num_views: int,
              num_points: int, distortion: bool, *, sufficient_decrease: float = 1e-4, curvature: float = 0.9,
              error_threshold: float = 1e-4, iterations: int = 1000, minimum_step: float = 1e-8,

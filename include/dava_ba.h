@@ -127,6 +127,19 @@ int dava_ba_solve(const DavaScene* scene, const DavaSolverConfig* config, const 
 int dava_ba_evaluate(const DavaScene* scene, const float* x, const float* direction, const float* alpha,
                      float* error_out, float* grad_out, float* slope_out, void* stream);
 
+/* Second derivatives of the objective, for differentiating THROUGH a solve whose error
+ * function is a fused objective (the reference's create_graph double backward,
+ * bfgs_solver.py:133-135).  Per problem, at x with direction v (per problem, NULL = 0):
+ *   error_out (B)         E
+ *   grad_out  (B, P)      dE/dx
+ *   hv_out    (B, P)      (d^2E/dx^2) v
+ *   obs_grad_out (B,M,N,2)  dE/dobs
+ *   obs_hv_out   (B,M,N,2)  (d^2E/dobs dx) v
+ * Every output may be NULL.  Forward-over-reverse of the same objective code (dual numbers).
+ * Shapes whose dual LDS image exceeds 160 KiB return DAVA_ERR_UNSUPPORTED.                 */
+int dava_ba_second_order(const DavaScene* scene, const float* x, const float* direction, float* error_out,
+                         float* grad_out, float* hv_out, float* obs_grad_out, float* obs_hv_out, void* stream);
+
 /* ---- generic BFGS building blocks (drive an arbitrary error closure) ----
  * batch = number of problems (all leading dims flattened), n = P.          */
 

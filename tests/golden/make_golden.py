@@ -314,6 +314,24 @@ def gen_solve_grad():
     out["ba_x0"], out["ba_obs"], out["ba_vis"], out["ba_w"] = (x0.detach().numpy(), obs.detach().numpy(),
                                                                 vis.numpy(), w.numpy())
     out["ba_out"], out["ba_grad"], out["ba_obs_grad"] = res.detach().numpy(), x0.grad.numpy(), obs.grad.numpy()
+    # fp32 versions (the fused objectives' dtype): squared reprojection and CalibrationNetwork's ray angle
+    for name, scenes_kw, objective in (("ba32", dict(seed=8103), ref_objective),
+                                       ("ray32", dict(seed=8104, ray_angle=True), ref_ray_angle)):
+        s = make_scenes(2, m, n, **scenes_kw)
+        x0 = torch.tensor(s.initial, requires_grad=True)
+        obs = torch.tensor(s.observations, requires_grad=True)
+        vis = torch.tensor(s.visibility)
+        w = torch.tensor(rng.normal(size=x0.shape), dtype=torch.float32)
+
+        def fn(p, mask, obs=obs, vis=vis, objective=objective):
+            return objective(p, obs[mask], vis[mask], m, n)
+
+        res = BFGSSolver(iterations=5, error_threshold=-1.0, minimum_step=-1.0).eval()(x0, fn)
+        (res * w).sum().backward()
+        out[name + "_x0"], out[name + "_obs"], out[name + "_vis"], out[name + "_w"] = (
+            x0.detach().numpy(), obs.detach().numpy(), vis.numpy(), w.numpy())
+        out[name + "_out"], out[name + "_grad"], out[name + "_obs_grad"] = (
+            res.detach().numpy(), x0.grad.numpy(), obs.grad.numpy())
     np.savez_compressed(os.path.join(HERE, "solve_grad.npz"), **out)
 
 

@@ -170,16 +170,6 @@ def test_output_does_not_require_grad_and_no_grad_block(device):
     assert sphere(out).item() <= 1e-6
 
 
-def test_requires_grad_with_a_fused_objective_is_refused_loudly(device):
-    """Second derivatives of the fused objective kernels are not implemented: refuse, never fall back."""
-    from deep_attention_visual_odometry_amd import ReprojectionError, make_scenes
-
-    s = make_scenes(1, 2, 8, seed=3)
-    fn = ReprojectionError(torch.tensor(s.observations, device=device), torch.tensor(s.visibility, device=device), 2, 8)
-    with pytest.raises(NotImplementedError):
-        _solver()(torch.tensor(s.initial, device=device, requires_grad=True), fn)
-
-
 def test_update_kat_textbook(device):
     """tests/autograd_solvers/test_bfgs_solver.py:307-332 known answer."""
     from deep_attention_visual_odometry_amd import BFGSSolver

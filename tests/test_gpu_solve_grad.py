@@ -174,3 +174,74 @@ def test_gradient_through_the_solve_matches_oracle_fp32_batch(device):
     (out * w.to(device)).sum().backward()
     assert _rel(out.detach().cpu(), ref.detach()) < 1e-5
     assert _rel(xd.grad.cpu(), xr.grad) < 1e-4
+
+
+# ---- second derivatives of the fused objectives (csrc/ba_second_order.hip) ----
+
+def _second_oracle(x, obs, vis, m, n, distortion, residual, v):
+    """H v and (d2E/dobs dx) v by torch double backward through the oracle, fp64."""
+    x64 = x.double().clone().requires_grad_(True)
+    o64 = obs.double().clone().requires_grad_(True)
+    if residual == "ray":
+        e = objective.ray_angle_error(x64, o64, vis, m, n)
+    else:
+        e = objective.reprojection_error(x64, o64, vis, m, n, distortion)
+    (og,) = torch.autograd.grad(e.sum(), o64, retain_graph=True)
+    (g,) = torch.autograd.grad(e.sum(), x64, create_graph=True)
+    gv = (g * v.double()).sum()
+    hv, ohv = torch.autograd.grad(gv, (x64, o64))
+    return g.detach(), hv, og, ohv
+
+
+@pytest.mark.parametrize("residual,distortion", [("sq", False), ("sq", True), ("ray", False)])
+@pytest.mark.parametrize("m,n", [(2, 64), (4, 256)])
+def test_second_order_kernel_matches_double_backward(device, residual, distortion, m, n):
+    from deep_attention_visual_odometry_amd import make_scenes, native_ops
+    from deep_attention_visual_odometry_amd._native import DAVA_RESIDUAL_RAY_ANGLE, DAVA_RESIDUAL_SQUARED_REPROJECTION
+
+    s = make_scenes(4, m, n, distortion=distortion, seed=41 + n, drop=0.0 if distortion else 0.1,
+                    ray_angle=residual == "ray")
+    x, obs, vis = torch.tensor(s.initial), torch.tensor(s.observations), torch.tensor(s.visibility)
+    v = torch.randn(x.shape, generator=torch.Generator().manual_seed(3)) * x.abs().clamp(min=0.1) * 1e-2
+    res = DAVA_RESIDUAL_RAY_ANGLE if residual == "ray" else DAVA_RESIDUAL_SQUARED_REPROJECTION
+    err, g, hv, og, ohv = native_ops.ba_second_order(x.to(device), obs.to(device), vis.to(device), m, n, distortion,
+                                                    direction=v.to(device), residual=res)
+    g_ref, hv_ref, og_ref, ohv_ref = _second_oracle(x, obs, vis, m, n, distortion, residual, v)
+    for b in range(4):
+        assert _rel(g[b].cpu(), g_ref[b]) < 1e-4, ("g", b)
+        assert _rel(hv[b].cpu(), hv_ref[b]) < 1e-3, ("hv", b)
+        assert _rel(og[b].cpu(), og_ref[b]) < 1e-4, ("obs grad", b)
+        assert _rel(ohv[b].cpu(), ohv_ref[b]) < 1e-3, ("obs hv", b)
+
+
+@pytest.mark.parametrize("name", ["ba32", "ray32"])
+def test_gradient_through_a_fused_objective_solve_matches_reference(device, name):
+    """BFGSSolver with ReprojectionError / RayAngleError as the closure and x0, obs requiring
+    grad: d loss/d x0 and d loss/d obs through K = 5 iterations vs the REAL reference's
+    autograd (fp32 on both sides; the GPU's reduction order differs, hence 1e-3)."""
+    from deep_attention_visual_odometry_amd import RayAngleError, ReprojectionError
+
+    g = np.load(os.path.join(GOLDEN, "solve_grad.npz"))
+    x0 = torch.tensor(g[name + "_x0"], device=device, requires_grad=True)
+    obs = torch.tensor(g[name + "_obs"], device=device, requires_grad=True)
+    vis = torch.tensor(g[name + "_vis"], device=device)
+    fn = ReprojectionError(obs, vis, 2, 8) if name == "ba32" else RayAngleError(obs, vis, 2, 8)
+    out = _solver(iterations=5, error_threshold=-1.0, minimum_step=-1.0).eval()(x0, fn)
+    assert out.requires_grad
+    (out * torch.tensor(g[name + "_w"], device=device)).sum().backward()
+    assert _rel(out.detach().cpu(), torch.tensor(g[name + "_out"])) < 1e-5
+    assert _rel(x0.grad.cpu(), torch.tensor(g[name + "_grad"])) < 1e-3
+    assert _rel(obs.grad.cpu(), torch.tensor(g[name + "_obs_grad"])) < 1e-3
+
+
+def test_fused_objective_first_order_obs_gradient(device):
+    """d E / d obs of the fused objective (first order, no solve)."""
+    from deep_attention_visual_odometry_amd import ReprojectionError, make_scenes
+
+    s = make_scenes(3, 2, 64, seed=5, drop=0.1)
+    x, obs, vis = torch.tensor(s.initial), torch.tensor(s.observations), torch.tensor(s.visibility)
+    od = obs.to(device).requires_grad_(True)
+    e = ReprojectionError(od, vis.to(device), 2, 64)(x.to(device), torch.ones(3, dtype=torch.bool, device=device))
+    (go,) = torch.autograd.grad(e.sum(), od)
+    _, _, og_ref, _ = _second_oracle(x, obs, vis, 2, 64, False, "sq", torch.zeros_like(x))
+    assert _rel(go.cpu(), og_ref) < 1e-4

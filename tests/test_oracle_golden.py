@@ -216,3 +216,18 @@ def test_camera_l1_error_and_gradient_match_reference_bitwise(case, dt):
     grad = camera_l1.l1_gradient(*args, **kw)
     assert np.array_equal(err.numpy(), g[key + "_error"])
     assert np.array_equal(grad.numpy(), g[key + "_gradient"])
+
+
+@pytest.mark.parametrize("name", ["ba32", "ray32"])
+def test_gradient_through_fp32_solves_matches_reference_bitwise(name):
+    g = _load("solve_grad.npz")
+    x0 = torch.tensor(g[name + "_x0"]).requires_grad_(True)
+    obs = torch.tensor(g[name + "_obs"]).requires_grad_(True)
+    vis = torch.tensor(g[name + "_vis"])
+    closure = objective.ReprojectionClosure if name == "ba32" else objective.RayAngleClosure
+    fn = closure(obs, vis, 2, 8)
+    out = solver.bfgs_solve(x0, fn, iterations=5, error_threshold=-1.0, minimum_step=-1.0)
+    (out * torch.tensor(g[name + "_w"])).sum().backward()
+    assert np.array_equal(out.detach().numpy(), g[name + "_out"])
+    assert np.array_equal(x0.grad.numpy(), g[name + "_grad"])
+    assert np.array_equal(obs.grad.numpy(), g[name + "_obs_grad"])
