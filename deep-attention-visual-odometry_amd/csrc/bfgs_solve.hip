@@ -217,6 +217,7 @@ __device__ __forceinline__ void dense_sweep(const Layout& L, int Pld, float* __r
 // a product H v costs 2 passes over 2 nh P floats instead of a P^2 sweep.
 // Pass 1: 4 dots per entry (s.y, w.y, s.g, w.g) -> coefficients in LDS.
 // Pass 2: a = H y and b = H g as coefficient-weighted sums of the rows.
+template <int U>  // column groups of both rows in flight per lane in pass 1
 __device__ __forceinline__ void compact_products(int P, int Pv, int nh, const float* __restrict__ S, const float* __restrict__ W,
                                  float* coef, const float* hrho, const float* hc, float gamma0, const float* g,
                                  const float* gp, float* a_out, float* b_out) {
@@ -227,16 +228,27 @@ __device__ __forceinline__ void compact_products(int P, int Pv, int nh, const fl
     const float* sr = S + (size_t)j * Pv;
     const float* wr = W + (size_t)j * Pv;
     float sy = 0.f, wy = 0.f, sg = 0.f, wg = 0.f;
-    for (int q = lane; q < G; q += kWave) {
-      const f4v s4 = *reinterpret_cast<const f4v*>(sr + 4 * q);
-      const f4v w4 = *reinterpret_cast<const f4v*>(wr + 4 * q);
+    auto dots = [&](int q, const f4v& s4, const f4v& w4) {
       const float4 g4 = ld4(g + 4 * q), p4 = ld4(gp + 4 * q);
       const float y0 = g4.x - p4.x, y1 = g4.y - p4.y, y2 = g4.z - p4.z, y3 = g4.w - p4.w;
       sy += s4[0] * y0 + s4[1] * y1 + s4[2] * y2 + s4[3] * y3;
       wy += w4[0] * y0 + w4[1] * y1 + w4[2] * y2 + w4[3] * y3;
       sg += s4[0] * g4.x + s4[1] * g4.y + s4[2] * g4.z + s4[3] * g4.w;
       wg += w4[0] * g4.x + w4[1] * g4.y + w4[2] * g4.z + w4[3] * g4.w;
+    };
+    int q = lane;
+    for (; q + (U - 1) * kWave < G; q += U * kWave) {
+      f4v s4[U], w4[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        s4[u] = *reinterpret_cast<const f4v*>(sr + 4 * (q + u * kWave));
+        w4[u] = *reinterpret_cast<const f4v*>(wr + 4 * (q + u * kWave));
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) dots(q + u * kWave, s4[u], w4[u]);
     }
+    for (; q < G; q += kWave)
+      dots(q, *reinterpret_cast<const f4v*>(sr + 4 * q), *reinterpret_cast<const f4v*>(wr + 4 * q));
     sy = wave_sum(sy); wy = wave_sum(wy); sg = wave_sum(sg); wg = wave_sum(wg);
     if (lane == 0) {
       const float rho = hrho[j], cr = hc[j] * rho;
@@ -515,7 +527,9 @@ __global__ __launch_bounds__(kBlock, DAVA_SOLVE_WAVES_PER_EU) void bfgs_ba_solve
           else if (GM == 4) compact_products_fused<4>(P, Pv, k - 1, SH, WH, hrho, hc, gamma0, g, gp, hy_new, hg, s_pend, hy_pend, d, hg);
           else
 #endif
-          compact_products(P, Pv, k - 1, SH, WH, hcoef, hrho, hc, gamma0, g, gp, hy_new, hg);
+          // GV mode (very long rows, few resident waves): 8 column groups in flight per lane;
+          // the LDS-mode kernel keeps the lean loop (its register budget is the fused pass's)
+          compact_products<GV ? 8 : 1>(P, Pv, k - 1, SH, WH, hcoef, hrho, hc, gamma0, g, gp, hy_new, hg);
         }
 #endif
         __syncthreads();

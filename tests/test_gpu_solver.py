@@ -290,3 +290,68 @@ def test_ray_angle_converges_from_noisy_guess(device):
     e1 = objective.ray_angle_error(out.double(), obs.double(), vis, 2, 64)
     assert (e1 < 1e-2 * e0).all(), (e0, e1)
     assert torch.isfinite(out).all()
+
+
+# ---- edge cases and error behaviour (raise, never fall back) ----
+
+def test_empty_batch_and_single_problem(device):
+    from deep_attention_visual_odometry_amd import BFGSSolver, ReprojectionError
+
+    x0, obs, vis = _scene(1, 2, 64, False, 501)
+    s = BFGSSolver(iterations=5, error_threshold=-1.0, minimum_step=-1.0).eval()
+    empty = s(x0[:0].to(device), ReprojectionError(obs[:0].to(device), vis[:0].to(device), 2, 64))
+    assert empty.shape == (0, x0.shape[1])
+    one = s(x0[0].to(device), ReprojectionError(obs[0].to(device), vis[0].to(device), 2, 64)).cpu()  # 0-d batch
+    fn = objective.ReprojectionClosure(obs, vis, 2, 64)
+    ref = solver.bfgs_solve(x0, fn, iterations=5, error_threshold=-1.0, minimum_step=-1.0)
+    assert one.shape == x0[0].shape
+    assert _rel(one[None], ref).max() <= TOL
+
+
+def test_non_contiguous_inputs_match_contiguous(device):
+    x0, obs, vis = _scene(4, 2, 64, False, 502)
+    out, _ = _gpu_solve(device, x0, obs, vis, 2, 64, False, iterations=10, error_threshold=-1.0, minimum_step=-1.0)
+    xs = torch.stack([x0, torch.zeros_like(x0)], dim=1).reshape(-1, x0.shape[1])[::2]  # strided rows
+    obs_t = obs.transpose(1, 2).contiguous().transpose(1, 2)  # non-contiguous view, same values
+    assert not obs_t.is_contiguous()
+    assert not xs.is_contiguous() and torch.equal(xs, x0)
+    out2, _ = _gpu_solve(device, xs, obs_t, vis, 2, 64, False, iterations=10, error_threshold=-1.0,
+                         minimum_step=-1.0)
+    assert torch.equal(out, out2)
+
+
+def test_bad_inputs_raise(device):
+    from deep_attention_visual_odometry_amd import BFGSSolver, RayAngleError, ReprojectionError
+
+    x0, obs, vis = _scene(2, 2, 64, False, 503)
+    with pytest.raises(ValueError):  # wrong observation shape
+        ReprojectionError(obs[:, :, :10].to(device), vis[:, :, :10].to(device), 2, 64)
+    fn = ReprojectionError(obs.to(device), vis.to(device), 2, 64)
+    with pytest.raises(ValueError):  # batch mismatch
+        BFGSSolver().eval()(x0[:1].to(device), fn)
+    with pytest.raises(TypeError):  # the fused path is fp32 (the reference's BA dtype)
+        BFGSSolver().eval()(x0.double().to(device), fn)
+    with pytest.raises(RuntimeError):  # no CPU fallback
+        BFGSSolver().eval()(x0, fn)
+    from deep_attention_visual_odometry_amd import native_ops
+    from deep_attention_visual_odometry_amd._native import DAVA_RESIDUAL_RAY_ANGLE
+
+    with pytest.raises(RuntimeError):  # ray angle is pinhole only: the library refuses the scene
+        native_ops.ba_evaluate(torch.zeros(1, 3 + 3 * 64 + 6 + 5, device=device),
+                               torch.zeros(1, 2, 64, 2, device=device), torch.ones(1, 2, 64, device=device), 2, 64,
+                               True, residual=DAVA_RESIDUAL_RAY_ANGLE)
+    assert RayAngleError(obs.to(device), vis.to(device), 2, 64).residual == DAVA_RESIDUAL_RAY_ANGLE
+
+
+def test_nan_problem_does_not_disturb_its_neighbours(device):
+    """Problems are independent: a NaN initial guess in one row (which the reference would
+    carry to NaN) leaves every other row's result identical to a clean run."""
+    x0, obs, vis = _scene(4, 2, 64, False, 504)
+    clean, _ = _gpu_solve(device, x0, obs, vis, 2, 64, False, iterations=10, error_threshold=-1.0,
+                          minimum_step=-1.0)
+    bad = x0.clone()
+    bad[1, 5] = float("nan")
+    out, _ = _gpu_solve(device, bad, obs, vis, 2, 64, False, iterations=10, error_threshold=-1.0,
+                        minimum_step=-1.0)
+    assert torch.equal(out[[0, 2, 3]], clean[[0, 2, 3]])
+    assert not torch.isfinite(out[1]).all()
