@@ -84,7 +84,7 @@ constexpr int kViewPart = 8;
 
 // LDS footprint helpers (floats)
 __host__ __device__ inline int views_floats(int M) { return (M - 1) * kViewStride; }
-__host__ __device__ inline int vpart_floats(int M) { return M * kWaves * kViewPart; }
+__host__ __device__ inline int vpart_floats(int M, int nw = kWaves) { return M * nw * kViewPart; }
 
 template <typename S>
 struct Intrinsics {
@@ -174,10 +174,11 @@ __device__ __forceinline__ void ray_angle_pair(const RayAngle<S>& ra, const floa
 //        after the first reduction without evaluating (the caller knows the answer:
 //        f(x) and phi'(0)); otherwise evaluate and return true.
 template <bool GRAD, bool SLOPE, bool TRIAL, bool DOT = false, bool CHECK = false,
-          int RES = DAVA_RESIDUAL_SQUARED_REPROJECTION, typename S = float>
+          int RES = DAVA_RESIDUAL_SQUARED_REPROJECTION, typename S = float, int NW = kWaves>
 __device__ __forceinline__ bool ba_eval(const Layout& L, const S* x, const S* d, float alpha, const float* obs,
                                         const uint8_t* vis, S* grad, S* views, S* vpart, float* scratch, int& buf,
                                         S& E_out, S& slope_out, S* obs_grad = nullptr) {
+  constexpr int BLOCK = kWave * NW;  // threads in the workgroup
   static_assert(!DOT || (GRAD && !SLOPE), "DOT derives the slope from the reverse-mode gradient");
   static_assert(!CHECK || TRIAL, "CHECK needs a trial point");
   const int tid = threadIdx.x;
@@ -186,7 +187,7 @@ __device__ __forceinline__ bool ba_eval(const Layout& L, const S* x, const S* d,
   const int M = L.M, N = L.N;
 
   // 1. per-view rotation constants (views 1..M-1), one thread per view
-  for (int m = 1 + tid; m < M; m += kBlock) {
+  for (int m = 1 + tid; m < M; m += BLOCK) {
     S* v = views + (m - 1) * kViewStride;
     const int r = L.rot(m), t = L.tr(m);
     const S w0 = trial_value<TRIAL>(x, d, alpha, r + 0);
@@ -214,7 +215,7 @@ __device__ __forceinline__ bool ba_eval(const Layout& L, const S* x, const S* d,
   // 2. scale normalisation s = (mean|X| N + mean|t| M)/(N+M), and its slope
   S sums[3] = {0.f, 0.f, 0.f};  // sum|X|, sum sgn(X) dX (SLOPE or DOT), moved (CHECK)
   bool moved = false;
-  for (int n = tid; n < N; n += kBlock) {
+  for (int n = tid; n < N; n += BLOCK) {
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
       const S X = trial_value<TRIAL>(x, d, alpha, L.pt(n) + c);
@@ -226,16 +227,16 @@ __device__ __forceinline__ bool ba_eval(const Layout& L, const S* x, const S* d,
   if constexpr (CHECK) {
     // the parameters that are not point coordinates: intrinsics, views, distortion
     const int other = L.P - 3 * N;
-    for (int k = tid; k < other; k += kBlock) {
+    for (int k = tid; k < other; k += BLOCK) {
       const int i = k < 3 ? k : k + 3 * N;
       moved |= trial_value<true>(x, d, alpha, i) != x[i];
     }
     sums[2] = moved ? 1.f : 0.f;
-    block_sum<3>(sums, scratch, buf);
+    block_sum<3, NW>(sums, scratch, buf);
   } else if constexpr (SLOPE || DOT) {
-    block_sum<2>(reinterpret_cast<S(&)[2]>(sums), scratch, buf);
+    block_sum<2, NW>(reinterpret_cast<S(&)[2]>(sums), scratch, buf);
   } else {
-    block_sum<1>(reinterpret_cast<S(&)[1]>(sums), scratch, buf);
+    block_sum<1, NW>(reinterpret_cast<S(&)[1]>(sums), scratch, buf);
   }
   buf ^= 1;  // (this barrier also publishes the view constants)
   if constexpr (CHECK) {
@@ -311,7 +312,7 @@ __device__ __forceinline__ bool ba_eval(const Layout& L, const S* x, const S* d,
     }
     S vg[7] = {0, 0, 0, 0, 0, 0, 0};  // gw_direct xyz, g_theta, g_t~ xyz
 
-    for (int n = tid; n < N; n += kBlock) {
+    for (int n = tid; n < N; n += BLOCK) {
       const int ip = L.pt(n);
       const S X0 = trial_value<TRIAL>(x, d, alpha, ip + 0);
       const S X1 = trial_value<TRIAL>(x, d, alpha, ip + 1);
@@ -461,7 +462,7 @@ __device__ __forceinline__ bool ba_eval(const Layout& L, const S* x, const S* d,
 #pragma unroll
         for (int k = 0; k < 7; ++k) {
           const S w = wave_sum(vg[k]);
-          if (lane == 0) vpart[(m * kWaves + wave) * kViewPart + k] = w;
+          if (lane == 0) vpart[(m * NW + wave) * kViewPart + k] = w;
         }
       }
     }
@@ -470,8 +471,8 @@ __device__ __forceinline__ bool ba_eval(const Layout& L, const S* x, const S* d,
   // 5. block reduction of error, slope, intrinsics gradient and scale-path sum
   if constexpr (GRAD) {
     S r[12] = {e_loc, sl_loc, gin[0], gin[1], gin[2], gin[3], gin[4], gin[5], gin[6], gin[7], gsx, gdx};
-    if constexpr (DOT) block_sum<12>(r, scratch, buf);
-    else block_sum<11>(reinterpret_cast<S(&)[11]>(r), scratch, buf);
+    if constexpr (DOT) block_sum<12, NW>(r, scratch, buf);
+    else block_sum<11, NW>(reinterpret_cast<S(&)[11]>(r), scratch, buf);
     buf ^= 1;
     E_out = r[0];
     slope_out = r[1];
@@ -481,8 +482,8 @@ __device__ __forceinline__ bool ba_eval(const Layout& L, const S* x, const S* d,
       const S* v = views + (m - 1) * kViewStride;
 #pragma unroll
       for (int c = 0; c < 3; ++c) {
-        const S* q = vpart + (m * kWaves) * kViewPart + 4 + c;
-        const S g = ((q[0] + q[kViewPart]) + q[2 * kViewPart]) + q[3 * kViewPart];
+        const S* q = vpart + (m * NW) * kViewPart + 4 + c;
+        const S g = wave_partials_total<NW>(q, kViewPart);
         gst += g * v[VT0 + c];
       }
     }
@@ -496,8 +497,8 @@ __device__ __forceinline__ bool ba_eval(const Layout& L, const S* x, const S* d,
       for (int m = 1; m < M; ++m) {
         const S* v = views + (m - 1) * kViewStride;
         auto vs = [&](int k) {
-          const S* p = vpart + (m * kWaves) * kViewPart + k;
-          return ((p[0] + p[kViewPart]) + p[2 * kViewPart]) + p[3 * kViewPart];
+          const S* p = vpart + (m * NW) * kViewPart + k;
+          return wave_partials_total<NW>(p, kViewPart);
         };
         const S gth = vs(3) * v[VRCP];
 #pragma unroll
@@ -513,7 +514,7 @@ __device__ __forceinline__ bool ba_eval(const Layout& L, const S* x, const S* d,
       }
       slope_out = (r[11] * inv_s + gabsX * sums[1]) + dv + di;
     }
-    for (int n = tid; n < N; n += kBlock) {
+    for (int n = tid; n < N; n += BLOCK) {
       S* gp = grad + L.pt(n);
 #pragma unroll
       for (int c = 0; c < 3; ++c) {
@@ -521,12 +522,12 @@ __device__ __forceinline__ bool ba_eval(const Layout& L, const S* x, const S* d,
         gp[c] = gp[c] * inv_s + sgn(X) * gabsX;
       }
     }
-    for (int q = tid; q < 6 * (M - 1); q += kBlock) {
+    for (int q = tid; q < 6 * (M - 1); q += BLOCK) {
       const int m = 1 + q / 6, c = q % 6;
       const S* v = views + (m - 1) * kViewStride;
       auto vsum = [&](int k) {
-        const S* p = vpart + (m * kWaves) * kViewPart + k;
-        return ((p[0] + p[kViewPart]) + p[2 * kViewPart]) + p[3 * kViewPart];
+        const S* p = vpart + (m * NW) * kViewPart + k;
+        return wave_partials_total<NW>(p, kViewPart);
       };
       if (c < 3) {
         grad[L.tr(m) + c] = vsum(4 + c) * inv_s + sgn(v[VT0 + c]) * gabsT;
@@ -545,8 +546,8 @@ __device__ __forceinline__ bool ba_eval(const Layout& L, const S* x, const S* d,
     __syncthreads();
   } else {
     S r[2] = {e_loc, sl_loc};
-    if constexpr (SLOPE) block_sum<2>(r, scratch, buf);
-    else block_sum<1>(reinterpret_cast<S(&)[1]>(r), scratch, buf);
+    if constexpr (SLOPE) block_sum<2, NW>(r, scratch, buf);
+    else block_sum<1, NW>(reinterpret_cast<S(&)[1]>(r), scratch, buf);
     buf ^= 1;
     E_out = r[0];
     slope_out = r[1];

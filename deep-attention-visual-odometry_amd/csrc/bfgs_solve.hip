@@ -49,7 +49,12 @@ struct LdsCarve {
   int x, d, g0, g1, s0, s1, hy0, hy1, hg, obs, views, vpart, scratch, hcoef, hrho, hc, vis_bytes_off, total_bytes;
 };
 
-constexpr int kVectors = 9;  // x d g g_prev s s_pend Hy Hy_pend Hg
+constexpr int kVectors = 9;
+
+// Waves per solve workgroup: 4 when the problem lives in LDS (two workgroups per CU);
+// 8 in global-vector mode, where problems are few and long (C5: B = 256 on 256 CUs) and
+// one workgroup per CU would otherwise leave each SIMD a single wave to hide latency with.
+__host__ __device__ constexpr int solve_waves(bool gv) { return gv ? 8 : 4; }  // x d g g_prev s s_pend Hy Hy_pend Hg
 
 // LDS image of one problem.  In global-vector (GV) mode -- large P, where the O(P)
 // vectors cannot live on-chip -- the nine vectors sit in a per-problem slice of the
@@ -70,8 +75,8 @@ __host__ __device__ inline LdsCarve carve_lds(int M, int N, int Pv, int kcap = 0
   c.hg = o; o += Pv;
   c.obs = off; off += gv ? 0 : round_up(2 * M * N, 4);
   c.views = off; off += round_up(views_floats(M), 4);
-  c.vpart = off; off += round_up(vpart_floats(M), 4);
-  c.scratch = off; off += 2 * kWaves * 32;
+  c.vpart = off; off += round_up(vpart_floats(M, solve_waves(gv)), 4);
+  c.scratch = off; off += 2 * solve_waves(gv) * 32;
   c.hcoef = off; off += 4 * kcap;  // COMPACT: per-entry product coefficients
   c.hrho = off; off += round_up(kcap, 4);
   c.hc = off; off += round_up(kcap, 4);
@@ -144,6 +149,7 @@ __device__ __forceinline__ float rank2(float h, float sri, float sj, float c, fl
 // access is a contiguous row piece of up to 1 KiB.  Lane = column means the
 // column sums need no cross-lane reduction.  U rows are loaded before any is
 // consumed to keep U KiB per wave in flight.
+template <int NW>
 __device__ __forceinline__ void dense_sweep(const Layout& L, int Pld, float* __restrict__ H, bool materialized, float gamma0,
                             const float* ps, const float* phy, float prho, float pc, const float* g,
                             const float* gp, float* hy_out, float* hg_out) {
@@ -152,7 +158,7 @@ __device__ __forceinline__ void dense_sweep(const Layout& L, int Pld, float* __r
   const int lane = threadIdx.x & (kWave - 1);
   const int wave = threadIdx.x / kWave;
   const int G = (P + 3) / 4;                      // float4 column groups
-  const int Gw = (G + kWaves - 1) / kWaves;       // groups per wave
+  const int Gw = (G + NW - 1) / NW;       // groups per wave
   const int g_end = min(G, (wave + 1) * Gw);
   for (int gb = wave * Gw; gb < g_end; gb += kWave) {
     const int grp = gb + lane;
@@ -217,14 +223,14 @@ __device__ __forceinline__ void dense_sweep(const Layout& L, int Pld, float* __r
 // a product H v costs 2 passes over 2 nh P floats instead of a P^2 sweep.
 // Pass 1: 4 dots per entry (s.y, w.y, s.g, w.g) -> coefficients in LDS.
 // Pass 2: a = H y and b = H g as coefficient-weighted sums of the rows.
-template <int U>  // column groups of both rows in flight per lane in pass 1
+template <int U, int NW>  // U: column groups of both rows in flight per lane in pass 1
 __device__ __forceinline__ void compact_products(int P, int Pv, int nh, const float* __restrict__ S, const float* __restrict__ W,
                                  float* coef, const float* hrho, const float* hc, float gamma0, const float* g,
                                  const float* gp, float* a_out, float* b_out) {
   const int lane = threadIdx.x & (kWave - 1);
   const int wave = threadIdx.x / kWave;
   const int G = (P + 3) / 4;
-  for (int j = wave; j < nh; j += kWaves) {
+  for (int j = wave; j < nh; j += NW) {
     const float* sr = S + (size_t)j * Pv;
     const float* wr = W + (size_t)j * Pv;
     float sy = 0.f, wy = 0.f, sg = 0.f, wg = 0.f;
@@ -259,7 +265,7 @@ __device__ __forceinline__ void compact_products(int P, int Pv, int nh, const fl
     }
   }
   __syncthreads();
-  for (int q = threadIdx.x; q < G; q += kBlock) {
+  for (int q = threadIdx.x; q < G; q += (kWave * NW)) {
     const float4 g4 = ld4(g + 4 * q), p4 = ld4(gp + 4 * q);
     f4v y4 = {g4.x - p4.x, g4.y - p4.y, g4.z - p4.z, g4.w - p4.w};
     f4v gg = {g4.x, g4.y, g4.z, g4.w};
@@ -410,7 +416,9 @@ __device__ __forceinline__ void compact_products_fused(int P, int Pv, int nh, co
 }
 
 template <int MODE, bool GV, int RES>
-__global__ __launch_bounds__(kBlock, DAVA_SOLVE_WAVES_PER_EU) void bfgs_ba_solve_kernel(SolveArgs a) {
+__global__ __launch_bounds__(kWave * solve_waves(GV), DAVA_SOLVE_WAVES_PER_EU) void bfgs_ba_solve_kernel(SolveArgs a) {
+  constexpr int NW = solve_waves(GV);
+  constexpr int BLOCK = kWave * NW;
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const Layout L = a.L;
   const int P = L.P, M = L.M, N = L.N;
@@ -440,7 +448,7 @@ __global__ __launch_bounds__(kBlock, DAVA_SOLVE_WAVES_PER_EU) void bfgs_ba_solve
 
   // ---- stage the problem into LDS (zero the vector pads) ----
   const float* x0 = a.x0 + (size_t)b * P;
-  for (int i = tid; i < Pv; i += kBlock) {
+  for (int i = tid; i < Pv; i += BLOCK) {
     x[i] = i < P ? x0[i] : 0.f;
     d[i] = g[i] = gp[i] = s_cur[i] = s_pend[i] = hy_new[i] = hy_pend[i] = hg[i] = 0.f;
   }
@@ -448,9 +456,9 @@ __global__ __launch_bounds__(kBlock, DAVA_SOLVE_WAVES_PER_EU) void bfgs_ba_solve
     float* o = lds + cv.obs;
     uint8_t* v = reinterpret_cast<uint8_t*>(lds) + cv.vis_bytes_off;
     const float* ob = a.obs + (size_t)b * 2 * MN;
-    for (int i = tid; i < 2 * MN; i += kBlock) o[i] = ob[i];
+    for (int i = tid; i < 2 * MN; i += BLOCK) o[i] = ob[i];
     const uint8_t* vbb = a.vis + (size_t)b * MN;
-    for (int i = tid; i < MN; i += kBlock) v[i] = vbb[i] ? 1 : 0;
+    for (int i = tid; i < MN; i += BLOCK) v[i] = vbb[i] ? 1 : 0;
   }
   __syncthreads();
 
@@ -479,7 +487,7 @@ __global__ __launch_bounds__(kBlock, DAVA_SOLVE_WAVES_PER_EU) void bfgs_ba_solve
     if (have_next) {
       E = E_next;
     } else {
-      ba_eval<true, false, false, false, false, RES, float>(L, x, nullptr, 0.f, obs, vis, g, views, vpart, scratch, buf, E,
+      ba_eval<true, false, false, false, false, RES, float, NW>(L, x, nullptr, 0.f, obs, vis, g, views, vpart, scratch, buf, E,
                                                      unused);
       ++evals;
     }
@@ -487,25 +495,25 @@ __global__ __launch_bounds__(kBlock, DAVA_SOLVE_WAVES_PER_EU) void bfgs_ba_solve
 
     if (k == 0) {
       // first step: no inverse Hessian yet, d = -g (bfgs_solver.py:152-155)
-      for (int i = tid; i < P; i += kBlock) d[i] = -1.0f * g[i];
+      for (int i = tid; i < P; i += BLOCK) d[i] = -1.0f * g[i];
       __syncthreads();
     } else {
       float r[4] = {0, 0, 0, 0};
       float rho, c, sg, hyg;
       if (k == 1) {
         // H_0 = gamma I, gamma from N&W eq. 6.20 (bfgs_solver.py:159-167, 217-233)
-        for (int i = tid; i < P; i += kBlock) {
+        for (int i = tid; i < P; i += BLOCK) {
           const float gi = g[i], yi = gi - gp[i], si = s_cur[i];
           r[0] += si * yi; r[1] += yi * yi; r[2] += si * gi; r[3] += yi * gi;
         }
-        block_sum<4>(r, scratch, buf); buf ^= 1;
+        block_sum<4, NW>(r, scratch, buf); buf ^= 1;
         const float gamma = clamp_min(r[0] / clamp_min(r[1], 1e-5f), 1e-4f);
         gamma0 = gamma;
         rho = r[0] <= 0.f ? 0.f : 1.0f / r[0];
         c = 1.0f + rho * (gamma * r[1]);
         sg = r[2];
         hyg = gamma * r[3];
-        for (int i = tid; i < P; i += kBlock) {
+        for (int i = tid; i < P; i += BLOCK) {
           const float gi = g[i], yi = gi - gp[i];
           hy_new[i] = gamma * yi;
           hg[i] = gamma * gi;
@@ -513,14 +521,17 @@ __global__ __launch_bounds__(kBlock, DAVA_SOLVE_WAVES_PER_EU) void bfgs_ba_solve
         // (no barrier needed: each thread reads back only its own hy_new / hg below)
       } else {
 #if DAVA_DIAG_NO_SWEEP  // timing-only build: H stays gamma0 I (results are wrong)
-        for (int i = tid; i < P; i += kBlock) { hy_new[i] = gamma0 * (g[i] - gp[i]); hg[i] = gamma0 * g[i]; }
+        for (int i = tid; i < P; i += BLOCK) { hy_new[i] = gamma0 * (g[i] - gp[i]); hg[i] = gamma0 * g[i]; }
 #else
         if constexpr (MODE == DAVA_HESSIAN_DENSE) {
-          dense_sweep(L, a.Pld, H, materialized, gamma0, s_pend, hy_pend, pend_rho, pend_c, g, gp, hy_new, hg);
+          dense_sweep<NW>(L, a.Pld, H, materialized, gamma0, s_pend, hy_pend, pend_rho, pend_c, g, gp, hy_new, hg);
           materialized = true;
         } else {
 #ifndef DAVA_COMPACT_TWO_PASS
           const int GM = ((P + 3) / 4 + kWave - 1) / kWave;
+          if constexpr (NW != kWaves) {  // the single pass's fixed 4-wave combine tree
+            compact_products<GV ? 8 : 1, NW>(P, Pv, k - 1, SH, WH, hcoef, hrho, hc, gamma0, g, gp, hy_new, hg);
+          } else
           if (GM <= 1) compact_products_fused<1>(P, Pv, k - 1, SH, WH, hrho, hc, gamma0, g, gp, hy_new, hg, s_pend, hy_pend, d, hg);
           else if (GM == 2) compact_products_fused<2>(P, Pv, k - 1, SH, WH, hrho, hc, gamma0, g, gp, hy_new, hg, s_pend, hy_pend, d, hg);
           else if (GM == 3) compact_products_fused<3>(P, Pv, k - 1, SH, WH, hrho, hc, gamma0, g, gp, hy_new, hg, s_pend, hy_pend, d, hg);
@@ -529,15 +540,15 @@ __global__ __launch_bounds__(kBlock, DAVA_SOLVE_WAVES_PER_EU) void bfgs_ba_solve
 #endif
           // GV mode (very long rows, few resident waves): 8 column groups in flight per lane;
           // the LDS-mode kernel keeps the lean loop (its register budget is the fused pass's)
-          compact_products<GV ? 8 : 1>(P, Pv, k - 1, SH, WH, hcoef, hrho, hc, gamma0, g, gp, hy_new, hg);
+          compact_products<GV ? 8 : 1, NW>(P, Pv, k - 1, SH, WH, hcoef, hrho, hc, gamma0, g, gp, hy_new, hg);
         }
 #endif
         __syncthreads();
-        for (int i = tid; i < P; i += kBlock) {
+        for (int i = tid; i < P; i += BLOCK) {
           const float gi = g[i], yi = gi - gp[i], si = s_cur[i], hi = hy_new[i];
           r[0] += si * yi; r[1] += hi * yi; r[2] += si * gi; r[3] += hi * gi;
         }
-        block_sum<4>(r, scratch, buf); buf ^= 1;
+        block_sum<4, NW>(r, scratch, buf); buf ^= 1;
         rho = r[0] <= 0.f ? 0.f : 1.0f / r[0];  // inverse_curvature (func_inverse_curvature.py:24-28)
         c = 1.0f + rho * r[1];
         sg = r[2];
@@ -545,7 +556,7 @@ __global__ __launch_bounds__(kBlock, DAVA_SOLVE_WAVES_PER_EU) void bfgs_ba_solve
       }
       // d = -H_k g,  H_k = H' + c (rho s) s^T - (rho s) (H'y)^T - (H'y) (rho s)^T
       const float rsg = rho * sg;
-      for (int i = tid; i < P; i += kBlock) {
+      for (int i = tid; i < P; i += BLOCK) {
         const float sri = s_cur[i] * rho;
         d[i] = -1.0f * (hg[i] + sri * (c * sg) - sri * hyg - hy_new[i] * rsg);
       }
@@ -559,7 +570,7 @@ __global__ __launch_bounds__(kBlock, DAVA_SOLVE_WAVES_PER_EU) void bfgs_ba_solve
         // append U_k = (s, H y, rho, c) to the history (entry k-1)
         float* sr = SH + (size_t)(k - 1) * Pv;
         float* wr = WH + (size_t)(k - 1) * Pv;
-        for (int i = tid; i < Pv; i += kBlock) { sr[i] = s_cur[i]; wr[i] = hy_new[i]; }
+        for (int i = tid; i < Pv; i += BLOCK) { sr[i] = s_cur[i]; wr[i] = hy_new[i]; }
         if (tid == 0) { hrho[k - 1] = rho; hc[k - 1] = c; }
       }
       __syncthreads();
@@ -569,8 +580,8 @@ __global__ __launch_bounds__(kBlock, DAVA_SOLVE_WAVES_PER_EU) void bfgs_ba_solve
     float dphi0;
     {
       float r[1] = {0.f};
-      for (int i = tid; i < P; i += kBlock) r[0] += d[i] * g[i];
-      block_sum<1>(r, scratch, buf); buf ^= 1;
+      for (int i = tid; i < P; i += BLOCK) r[0] += d[i] * g[i];
+      block_sum<1, NW>(r, scratch, buf); buf ^= 1;
       dphi0 = r[0];
     }
     float a_lo = 0.f, a_hi = 0.f, al = 1.f, f_lo = E, f_hi = E, fa = E, dfa = dphi0;
@@ -590,7 +601,7 @@ __global__ __launch_bounds__(kBlock, DAVA_SOLVE_WAVES_PER_EU) void bfgs_ba_solve
       // phi'(0).  The check rides on the objective's first reduction (CHECK).  Otherwise
       // E and the full gradient at the trial point are formed (kept for reuse as the
       // next iterate's gradient) and phi'(alpha) = d . grad (DOT).
-      if (ba_eval<true, !DAVA_TRIAL_DOT, true, DAVA_TRIAL_DOT, DAVA_TRIAL_CHECK, RES, float>(L, x, d, al, obs, vis, gp, views, vpart,
+      if (ba_eval<true, !DAVA_TRIAL_DOT, true, DAVA_TRIAL_DOT, DAVA_TRIAL_CHECK, RES, float, NW>(L, x, d, al, obs, vis, gp, views, vpart,
                                                                      scratch, buf, fa, dfa)) {
         ++evals;
         last_same = false;
@@ -632,19 +643,19 @@ __global__ __launch_bounds__(kBlock, DAVA_SOLVE_WAVES_PER_EU) void bfgs_ba_solve
     have_next = evaluated && last_al == alpha;
     E_next = last_fa;
     if (have_next && last_same) {  // x_{k+1} == x_k bitwise: its gradient is g itself
-      for (int i = tid; i < P; i += kBlock) gp[i] = g[i];
+      for (int i = tid; i < P; i += BLOCK) gp[i] = g[i];
     }
 
     // ---- take the step (bfgs_solver.py:191-199) and test its length (:203-207) ----
     {
       float r[1] = {0.f};
-      for (int i = tid; i < P; i += kBlock) {
+      for (int i = tid; i < P; i += BLOCK) {
         const float si = __fmul_rn(alpha, d[i]);
         s_cur[i] = si;
         x[i] = __fadd_rn(x[i], si);
         r[0] += si * si;
       }
-      block_sum<1>(r, scratch, buf); buf ^= 1;
+      block_sum<1, NW>(r, scratch, buf); buf ^= 1;
       ++steps;
       if (!(sqrtf(r[0]) > a.min_step)) { reason = DAVA_STOP_STEP; break; }
     }
@@ -653,10 +664,10 @@ __global__ __launch_bounds__(kBlock, DAVA_SOLVE_WAVES_PER_EU) void bfgs_ba_solve
   // ---- outputs ----
   __syncthreads();
   float* xo = a.x_out + (size_t)b * P;
-  for (int i = tid; i < P; i += kBlock) xo[i] = x[i];
+  for (int i = tid; i < P; i += BLOCK) xo[i] = x[i];
   if (a.err_out) {
     float e2 = 0.f;
-    ba_eval<false, false, false, false, false, RES, float>(L, x, nullptr, 0.f, obs, vis, nullptr, views, vpart, scratch, buf,
+    ba_eval<false, false, false, false, false, RES, float, NW>(L, x, nullptr, 0.f, obs, vis, nullptr, views, vpart, scratch, buf,
                                                    e2, unused);
     if (tid == 0) a.err_out[b] = e2;
   }
@@ -793,7 +804,7 @@ static void launch_solve_res(const SolveArgs& a, int B, int lds, hipStream_t s) 
   if (lds > 64 * 1024)
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(bfgs_ba_solve_kernel<MODE, GV, RES>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-  hipLaunchKernelGGL((bfgs_ba_solve_kernel<MODE, GV, RES>), dim3(B), dim3(kBlock), lds, s, a);
+  hipLaunchKernelGGL((bfgs_ba_solve_kernel<MODE, GV, RES>), dim3(B), dim3(kWave * solve_waves(GV)), lds, s, a);
 }
 
 template <int MODE, bool GV>

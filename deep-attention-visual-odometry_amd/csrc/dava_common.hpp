@@ -52,14 +52,14 @@ __device__ __forceinline__ float wave_sum<float>(float v) {
 // partials are added in a fixed order by every thread, so all threads hold
 // bit-identical results (the solver's control flow depends on them being
 // uniform).  `scratch` is double-buffered by the caller (alternate `buf`),
-// so ONE barrier per reduction suffices: a wave cannot reach the next use of
+// so ONE barrier per reduction suffices (NW = waves in the workgroup): a wave cannot reach the next use of
 // the same buffer before every wave has passed the intervening reduction's
 // barrier, i.e. before every wave finished reading this one.
-template <int R>
+template <int R, int NW = kWaves>
 __device__ __forceinline__ void block_sum(float (&v)[R], float* scratch, int buf) {
   const int lane = threadIdx.x & (kWave - 1);
   const int wave = threadIdx.x / kWave;
-  float* s = scratch + buf * (kWaves * 32);
+  float* s = scratch + buf * (NW * 32);
 #pragma unroll
   for (int r = 0; r < R; ++r) {
     float w = wave_sum(v[r]);
@@ -67,7 +67,21 @@ __device__ __forceinline__ void block_sum(float (&v)[R], float* scratch, int buf
   }
   __syncthreads();
 #pragma unroll
-  for (int r = 0; r < R; ++r) v[r] = ((s[r] + s[32 + r]) + s[64 + r]) + s[96 + r];
+  for (int r = 0; r < R; ++r) {
+    float t = s[r];  // wave partials added in wave order
+#pragma unroll
+    for (int w = 1; w < NW; ++w) t += s[w * 32 + r];
+    v[r] = t;
+  }
+}
+
+// Sum of NW per-wave partials stored `stride` apart, in wave order.
+template <int NW, typename T>
+__device__ __forceinline__ T wave_partials_total(const T* p, int stride) {
+  T t = p[0];
+#pragma unroll
+  for (int w = 1; w < NW; ++w) t += p[w * stride];
+  return t;
 }
 
 }  // namespace dava

@@ -92,10 +92,10 @@ __device__ __forceinline__ Dual wave_sum<Dual>(Dual x) {
 }
 
 // block_sum over R duals = block_sum over the 2R floats they are made of
-template <int R>
+template <int R, int NW = kWaves>
 __device__ __forceinline__ void block_sum(Dual (&v)[R], float* scratch, int buf) {
   static_assert(2 * R <= 32, "scratch rows hold 32 floats");
-  block_sum<2 * R>(reinterpret_cast<float(&)[2 * R]>(v), scratch, buf);
+  block_sum<2 * R, NW>(reinterpret_cast<float(&)[2 * R]>(v), scratch, buf);
 }
 
 }  // namespace dava
