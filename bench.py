@@ -68,13 +68,14 @@ def dense_algorithmic_bytes(p: int, mn: int, iters: int) -> float:
 
 def compact_algorithmic_bytes(p: int, mn: int, iters: int) -> float:
     """Minimum HBM bytes of the compact-history algorithm for one problem (Pv = P rounded
-    up to 4 floats): iteration k >= 2 reads the k-1 history rows of S and W -- once
-    (8 (k-1) Pv) on the fused single-pass path used for P <= 1024, twice (dots, then the
-    weighted sums: 16 (k-1) Pv) on the two-pass path for larger P; iterations k = 1 .. K-1
-    append one S and one W row = 8 Pv; scene and x0 read once, x written once."""
+    up to 4 floats): iteration k >= 2 reads the k-1 history rows of S and W once
+    (8 (k-1) Pv; the single-pass kernels -- fused per wave for P <= 1024, workgroup-wide
+    in global-vector mode for P <= 14336 -- do exactly this, the two-pass fallback for
+    mid-size LDS-mode rows reads them twice and is charged the minimum all the same);
+    iterations k = 1 .. K-1 append one S and one W row = 8 Pv; scene and x0 read once,
+    x written once."""
     pv = (p + 3) // 4 * 4
-    per_entry = 8.0 if (p + 3) // 4 <= 256 else 16.0
-    reads = per_entry * pv * sum(k - 1 for k in range(2, iters))
+    reads = 8.0 * pv * sum(k - 1 for k in range(2, iters))
     writes = 8.0 * pv * max(iters - 1, 0)
     return reads + writes + 9.0 * mn + 8.0 * p
 

@@ -49,12 +49,22 @@ struct LdsCarve {
   int x, d, g0, g1, s0, s1, hy0, hy1, hg, obs, views, vpart, scratch, hcoef, hrho, hc, vis_bytes_off, total_bytes;
 };
 
-constexpr int kVectors = 9;
+constexpr int kVectors = 9;  // x d g g_prev s s_pend Hy Hy_pend Hg
 
 // Waves per solve workgroup: 4 when the problem lives in LDS (two workgroups per CU);
 // 8 in global-vector mode, where problems are few and long (C5: B = 256 on 256 CUs) and
 // one workgroup per CU would otherwise leave each SIMD a single wave to hide latency with.
-__host__ __device__ constexpr int solve_waves(bool gv) { return gv ? 8 : 4; }  // x d g g_prev s s_pend Hy Hy_pend Hg
+__host__ __device__ constexpr int solve_waves(bool gv) { return gv ? 8 : 4; }
+
+// GV mode, COMPACT: the workgroup-wide single history pass keeps at most this many float4
+// column groups per thread in registers (P <= 7 * 512 * 4 = 14336); longer rows use two passes.
+#ifndef DAVA_WIDE_PASS
+#define DAVA_WIDE_PASS 1
+#endif
+constexpr int kWideMaxGroups = 7;
+__host__ __device__ inline bool wide_history_pass(int Pv, int kcap, bool gv) {
+  return DAVA_WIDE_PASS && gv && kcap > 0 && (Pv / 4 + kWave * solve_waves(gv) - 1) / (kWave * solve_waves(gv)) <= kWideMaxGroups;
+}
 
 // LDS image of one problem.  In global-vector (GV) mode -- large P, where the O(P)
 // vectors cannot live on-chip -- the nine vectors sit in a per-problem slice of the
@@ -299,6 +309,88 @@ __device__ __forceinline__ void compact_products(int P, int Pv, int nh, const fl
   }
 }
 
+// COMPACT mode, GV (long rows, 8-wave workgroup): one pass over the history, workgroup-wide.
+// Thread t owns float4 column groups t, t + 512, ... (GT of them) and keeps its columns of
+// y, g and of the two running sums in registers.  E entries per round (2 while GT <= 4, else
+// 1 so that s, w, y, g and the sums fit in 256 VGPRs): every thread loads its columns of the
+// entries' s and w rows, forms its partial dots with y and g, one block reduction gives the
+// 4E dots to every thread in the same order, and each thread adds the entries'
+// contributions to its own columns of H y and H g.  Rows cross HBM once per iteration (the
+// two-pass variant reads them twice).
+template <int GT, int NW>
+__device__ __forceinline__ void compact_products_wide(int P, int Pv, int nh, const float* __restrict__ S,
+                                                      const float* __restrict__ W, const float* hrho, const float* hc,
+                                                      float gamma0, const float* g, const float* gp, float* a_out,
+                                                      float* b_out, float* scratch, int& buf) {
+  constexpr int BLOCK = kWave * NW;
+  constexpr int E = GT <= 2 ? 2 : 1;
+  const int tid = threadIdx.x;
+  const int G = (P + 3) / 4;
+  const f4v z = f4v{0, 0, 0, 0};
+  f4v y[GT], gg[GT], pa[GT], pb[GT];
+#pragma unroll
+  for (int u = 0; u < GT; ++u) {
+    const int q = tid + u * BLOCK;
+    y[u] = gg[u] = pa[u] = pb[u] = z;
+    if (q < G) {
+      gg[u] = *reinterpret_cast<const f4v*>(g + 4 * q);
+      y[u] = gg[u] - *reinterpret_cast<const f4v*>(gp + 4 * q);
+    }
+  }
+  auto dot4 = [](f4v a, f4v b) { const f4v t = a * b; return (t[0] + t[1]) + (t[2] + t[3]); };
+  for (int j = 0; j < nh; j += E) {
+    const int ne = min(E, nh - j);  // uniform
+    f4v s4[E][GT], w4[E][GT];
+    float d[4 * E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+#pragma unroll
+      for (int u = 0; u < GT; ++u) {
+        const int q = tid + u * BLOCK;
+        s4[e][u] = w4[e][u] = z;
+        if (e < ne && q < G) {
+          s4[e][u] = *reinterpret_cast<const f4v*>(S + (size_t)(j + e) * Pv + 4 * q);
+          w4[e][u] = *reinterpret_cast<const f4v*>(W + (size_t)(j + e) * Pv + 4 * q);
+        }
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      d[4 * e] = d[4 * e + 1] = d[4 * e + 2] = d[4 * e + 3] = 0.0f;
+#pragma unroll
+      for (int u = 0; u < GT; ++u) {
+        d[4 * e] += dot4(s4[e][u], y[u]);
+        d[4 * e + 1] += dot4(w4[e][u], y[u]);
+        d[4 * e + 2] += dot4(s4[e][u], gg[u]);
+        d[4 * e + 3] += dot4(w4[e][u], gg[u]);
+      }
+    }
+    block_sum<4 * E, NW>(d, scratch, buf);
+    buf ^= 1;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      if (e < ne) {
+        const float rho = hrho[j + e], cr = hc[j + e] * rho;
+        const float ay = cr * d[4 * e] - rho * d[4 * e + 1], by = -rho * d[4 * e];
+        const float ag = cr * d[4 * e + 2] - rho * d[4 * e + 3], bg = -rho * d[4 * e + 2];
+#pragma unroll
+        for (int u = 0; u < GT; ++u) {
+          pa[u] += ay * s4[e][u] + by * w4[e][u];
+          pb[u] += ag * s4[e][u] + bg * w4[e][u];
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < GT; ++u) {
+    const int q = tid + u * BLOCK;
+    if (q < G) {
+      *reinterpret_cast<f4v*>(a_out + 4 * q) = pa[u] + gamma0 * y[u];
+      *reinterpret_cast<f4v*>(b_out + 4 * q) = pb[u] + gamma0 * gg[u];
+    }
+  }
+}
+
 // COMPACT mode, single pass (P <= 1024, i.e. at most GM <= 4 float4 groups per lane):
 // the coefficients of entry j depend only on entry j's own dots, so one wave
 // loads the two rows of an entry into registers, reduces its 4 dots in-wave
@@ -528,9 +620,20 @@ __global__ __launch_bounds__(kWave * solve_waves(GV), DAVA_SOLVE_WAVES_PER_EU) v
           materialized = true;
         } else {
 #ifndef DAVA_COMPACT_TWO_PASS
-          const int GM = ((P + 3) / 4 + kWave - 1) / kWave;
-          if constexpr (NW != kWaves) {  // the single pass's fixed 4-wave combine tree
-            compact_products<GV ? 8 : 1, NW>(P, Pv, k - 1, SH, WH, hcoef, hrho, hc, gamma0, g, gp, hy_new, hg);
+          const int G4 = (P + 3) / 4;
+          const int GM = (G4 + kWave - 1) / kWave;
+          if constexpr (NW != kWaves) {  // GV: workgroup-wide single pass, else two passes
+            const int GT = (G4 + kWave * NW - 1) / (kWave * NW);
+            const int nh = k - 1;
+            if (!wide_history_pass(Pv, a.kcap, GV))
+              compact_products<GV ? 8 : 1, NW>(P, Pv, nh, SH, WH, hcoef, hrho, hc, gamma0, g, gp, hy_new, hg);
+            else if (GT <= 1) compact_products_wide<1, NW>(P, Pv, nh, SH, WH, hrho, hc, gamma0, g, gp, hy_new, hg, scratch, buf);
+            else if (GT == 2) compact_products_wide<2, NW>(P, Pv, nh, SH, WH, hrho, hc, gamma0, g, gp, hy_new, hg, scratch, buf);
+            else if (GT == 3) compact_products_wide<3, NW>(P, Pv, nh, SH, WH, hrho, hc, gamma0, g, gp, hy_new, hg, scratch, buf);
+            else if (GT == 4) compact_products_wide<4, NW>(P, Pv, nh, SH, WH, hrho, hc, gamma0, g, gp, hy_new, hg, scratch, buf);
+            else if (GT == 5) compact_products_wide<5, NW>(P, Pv, nh, SH, WH, hrho, hc, gamma0, g, gp, hy_new, hg, scratch, buf);
+            else if (GT == 6) compact_products_wide<6, NW>(P, Pv, nh, SH, WH, hrho, hc, gamma0, g, gp, hy_new, hg, scratch, buf);
+            else compact_products_wide<7, NW>(P, Pv, nh, SH, WH, hrho, hc, gamma0, g, gp, hy_new, hg, scratch, buf);
           } else
           if (GM <= 1) compact_products_fused<1>(P, Pv, k - 1, SH, WH, hrho, hc, gamma0, g, gp, hy_new, hg, s_pend, hy_pend, d, hg);
           else if (GM == 2) compact_products_fused<2>(P, Pv, k - 1, SH, WH, hrho, hc, gamma0, g, gp, hy_new, hg, s_pend, hy_pend, d, hg);
