@@ -66,17 +66,18 @@ def dense_algorithmic_bytes(p: int, mn: int, iters: int) -> float:
     return h + 9.0 * mn + 8.0 * p
 
 
-def compact_algorithmic_bytes(p: int, mn: int, iters: int) -> float:
+def compact_algorithmic_bytes(p: int, mn: int, iters: int, lds_entries: int = 0) -> float:
     """Minimum HBM bytes of the compact-history algorithm for one problem (Pv = P rounded
     up to 4 floats): iteration k >= 2 reads the k-1 history rows of S and W once
     (8 (k-1) Pv; the single-pass kernels -- fused per wave for P <= 1024, workgroup-wide
     in global-vector mode for P <= 14336 -- do exactly this, the two-pass fallback for
     mid-size LDS-mode rows reads them twice and is charged the minimum all the same);
     iterations k = 1 .. K-1 append one S and one W row = 8 Pv; scene and x0 read once,
-    x written once."""
+    x written once.  The oldest `lds_entries` entries (dava_ba_solve_plan) never leave the
+    CU: they are neither written to nor read from HBM."""
     pv = (p + 3) // 4 * 4
-    reads = 8.0 * pv * sum(k - 1 for k in range(2, iters))
-    writes = 8.0 * pv * max(iters - 1, 0)
+    reads = 8.0 * pv * sum(max(k - 1 - lds_entries, 0) for k in range(2, iters))
+    writes = 8.0 * pv * max(iters - 1 - lds_entries, 0)
     return reads + writes + 9.0 * mn + 8.0 * p
 
 
@@ -192,8 +193,11 @@ def main():
     if rank == 0:
         headline = (b, args.views, args.points, distortion, ray, args.iterations) == (8192, 4, 256, True, False, 100)
         value = world * b * args.steps / elapsed
-        algo = b * (dense_algorithmic_bytes if args.mode == "dense" else compact_algorithmic_bytes)(
-            p, mn, args.iterations)
+        plan = native_ops.solve_plan(b, args.views, args.points, distortion, mode, args.iterations, residual)
+        if args.mode == "dense":
+            algo = b * dense_algorithmic_bytes(p, mn, args.iterations)
+        else:
+            algo = b * compact_algorithmic_bytes(p, mn, args.iterations, plan["lds_history_entries"])
         roofline = None
         if algo is not None:
             achieved = algo / (launch_ms * 1e-3) / 1e9
@@ -204,6 +208,8 @@ def main():
                 key = f"{args.mode}_B{b}_M{args.views}_N{args.points}_D{int(distortion)}_K{args.iterations}"
                 if ray:
                     key += "_ray"
+                if plan["lds_history_entries"]:
+                    key += f"_L{plan['lds_history_entries']}"
                 if key in tj:
                     traffic = tj[key]["hbm_bytes_per_launch"]
             except (OSError, ValueError, KeyError):
@@ -244,7 +250,7 @@ def main():
             "cpu_baseline": cpu,
             "diagnostics": {"objective_evals_per_iteration": round(evals, 3),
                             "line_search_trials_per_iteration": round(trials, 3),
-                            "all_finite": finite},
+                            "all_finite": finite, "plan": plan},
         }
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -42,11 +42,14 @@ struct SolveArgs {
   float c1, c2, thr, min_step;
   int iters, max_trials, strong, mode;
   int kcap;       // COMPACT: history capacity (entries)
+  int lcap;       // COMPACT, LDS mode: entries 0 .. lcap-1 live in LDS instead of HBM
   float* vecs;    // GV mode: B x kVectors x Pv floats (else unused)
+  unsigned long long* phase_cycles;  // DAVA_PHASE_TIMING builds: B x kPhases (else null)
 };
 
 struct LdsCarve {
-  int x, d, g0, g1, s0, s1, hy0, hy1, hg, obs, views, vpart, scratch, hcoef, hrho, hc, vis_bytes_off, total_bytes;
+  int x, d, g0, g1, s0, s1, hy0, hy1, hg, obs, views, vpart, scratch, hcoef, hrho, hc, hist, vis_bytes_off,
+      total_bytes;
 };
 
 constexpr int kVectors = 9;  // x d g g_prev s s_pend Hy Hy_pend Hg
@@ -69,7 +72,10 @@ __host__ __device__ inline bool wide_history_pass(int Pv, int kcap, bool gv) {
 // LDS image of one problem.  In global-vector (GV) mode -- large P, where the O(P)
 // vectors cannot live on-chip -- the nine vectors sit in a per-problem slice of the
 // workspace instead (offsets index that slice) and obs / vis are read in place.
-__host__ __device__ inline LdsCarve carve_lds(int M, int N, int Pv, int kcap = 0, bool gv = false) {
+// COMPACT LDS mode may keep the OLDEST lcap history entries on-chip (S row then W row,
+// 2 Pv floats per entry): entry j is read by every iteration k > j + 1, so the first
+// entries carry the most traffic (lcap = 6 at C3 removes 12% of the history reads).
+__host__ __device__ inline LdsCarve carve_lds(int M, int N, int Pv, int kcap = 0, bool gv = false, int lcap = 0) {
   LdsCarve c;
   int off = 0;
   int voff = 0;
@@ -90,6 +96,7 @@ __host__ __device__ inline LdsCarve carve_lds(int M, int N, int Pv, int kcap = 0
   c.hcoef = off; off += 4 * kcap;  // COMPACT: per-entry product coefficients
   c.hrho = off; off += round_up(kcap, 4);
   c.hc = off; off += round_up(kcap, 4);
+  c.hist = off; off += gv ? 0 : 2 * lcap * Pv;
   c.vis_bytes_off = off * 4;
   c.total_bytes = c.vis_bytes_off + (gv ? 0 : round_up(M * N, 16));
   return c;
@@ -123,6 +130,25 @@ __device__ __forceinline__ void st4(float* p, float4 v) { *reinterpret_cast<floa
 #endif
 #ifndef DAVA_SOLVE_WAVES_PER_EU
 #define DAVA_SOLVE_WAVES_PER_EU 2  // <= 256 VGPRs: two 4-wave workgroups per CU
+#endif
+// Diagnostic builds only (make variant FLAGS=-DDAVA_PHASE_TIMING=1): thread 0 of every
+// workgroup accumulates shader-clock cycles per solver phase; dava_ba_solve prints the
+// batch averages to stderr after the launch (and synchronises -- never in a product build).
+#ifndef DAVA_PHASE_TIMING
+#define DAVA_PHASE_TIMING 0
+#endif
+#if DAVA_PHASE_TIMING
+constexpr int kPhases = 7;  // eval at x, history products, direction, trial evals, search logic, step, total
+#define DAVA_PHASE(i)                          \
+  do {                                         \
+    const unsigned long long t1_ = clock64(); \
+    ph_acc[i] += t1_ - ph_t0;                  \
+    ph_t0 = t1_;                               \
+  } while (0)
+#else
+#define DAVA_PHASE(i) \
+  do {                \
+  } while (0)
 #endif
 
 // Streaming access to the inverse Hessian: every element is read once and
@@ -399,9 +425,13 @@ __device__ __forceinline__ void compact_products_wide(int P, int Pv, int nh, con
 // are dealt round-robin to the 4 waves; the per-wave partial sums are then
 // added in a fixed tree ((w0 + w2) + (w1 + w3)) through 4 spare LDS vectors,
 // so the result is deterministic.  a_out / b_out / spare0..3 are Pv-float LDS vectors.
+// Entries j < lcap are read from the LDS-resident history LH (S row at LH + 2 j Pv, W row
+// Pv floats later) -- the same values in the same per-wave order, so the result is
+// bitwise the same as with every entry in HBM.
 template <int GM>
 __device__ __forceinline__ void compact_products_fused(int P, int Pv, int nh, const float* __restrict__ S,
-                                       const float* __restrict__ W, const float* hrho, const float* hc,
+                                       const float* __restrict__ W, const float* LH, int lcap,
+                                       const float* hrho, const float* hc,
                                        float gamma0, const float* g, const float* gp, float* a_out, float* b_out,
                                        float* spare0, float* spare1, float* spare2, float* spare3) {
   const int lane = threadIdx.x & (kWave - 1);
@@ -456,6 +486,18 @@ __device__ __forceinline__ void compact_products_fused(int P, int Pv, int nh, co
     }
   };
   int j = wave;
+  for (const int nl = min(lcap, nh); j < nl; j += kWaves) {  // on-chip entries first (wave-uniform)
+    f4v s0[GM], w0[GM];
+    const float* sr = LH + (size_t)2 * j * Pv;
+    const float* wr = sr + Pv;
+#pragma unroll
+    for (int m = 0; m < GM; ++m) {
+      const int q = lane + kWave * m;
+      s0[m] = ok[m] ? *reinterpret_cast<const f4v*>(sr + 4 * q) : f4v{0, 0, 0, 0};
+      w0[m] = ok[m] ? *reinterpret_cast<const f4v*>(wr + 4 * q) : f4v{0, 0, 0, 0};
+    }
+    consume(j, s0, w0);
+  }
 #if DAVA_FUSED_PAIR
   for (; j + kWaves < nh; j += 2 * kWaves) {
     f4v s0[GM], w0[GM], s1[GM], w1[GM];
@@ -517,7 +559,9 @@ __global__ __launch_bounds__(kWave * solve_waves(GV), DAVA_SOLVE_WAVES_PER_EU) v
   const int Pv = a.Pv;
   const int b = blockIdx.x;
   const int tid = threadIdx.x;
-  const LdsCarve cv = carve_lds(M, N, Pv, MODE == DAVA_HESSIAN_COMPACT ? a.kcap : 0, GV);
+  const int lcap = MODE == DAVA_HESSIAN_COMPACT && !GV ? a.lcap : 0;
+  const LdsCarve cv = carve_lds(M, N, Pv, MODE == DAVA_HESSIAN_COMPACT ? a.kcap : 0, GV, lcap);
+  float* LH = lds + cv.hist;  // LDS-resident history entries 0 .. lcap-1
   float* vb0 = GV ? a.vecs + (size_t)b * kVectors * Pv : lds;
   float* x = vb0 + cv.x;
   float* d = vb0 + cv.d;
@@ -574,6 +618,11 @@ __global__ __launch_bounds__(kWave * solve_waves(GV), DAVA_SOLVE_WAVES_PER_EU) v
   // bit for bit, so the next iteration's objective + gradient are taken from it.
   bool have_next = false;
   float E_next = 0.f;
+#if DAVA_PHASE_TIMING
+  unsigned long long ph_acc[kPhases] = {0, 0, 0, 0, 0, 0, 0};
+  const unsigned long long ph_start = clock64();
+  unsigned long long ph_t0 = ph_start;
+#endif
   for (int k = 0; k < a.iters; ++k) {
     { float* t = g; g = gp; gp = t; }  // gp <- previous gradient; g <- (trial) gradient buffer
     if (have_next) {
@@ -583,6 +632,7 @@ __global__ __launch_bounds__(kWave * solve_waves(GV), DAVA_SOLVE_WAVES_PER_EU) v
                                                      unused);
       ++evals;
     }
+    DAVA_PHASE(0);
     if (!(E > a.thr)) { reason = DAVA_STOP_ERROR; break; }
 
     if (k == 0) {
@@ -635,10 +685,10 @@ __global__ __launch_bounds__(kWave * solve_waves(GV), DAVA_SOLVE_WAVES_PER_EU) v
             else if (GT == 6) compact_products_wide<6, NW>(P, Pv, nh, SH, WH, hrho, hc, gamma0, g, gp, hy_new, hg, scratch, buf);
             else compact_products_wide<7, NW>(P, Pv, nh, SH, WH, hrho, hc, gamma0, g, gp, hy_new, hg, scratch, buf);
           } else
-          if (GM <= 1) compact_products_fused<1>(P, Pv, k - 1, SH, WH, hrho, hc, gamma0, g, gp, hy_new, hg, s_pend, hy_pend, d, hg);
-          else if (GM == 2) compact_products_fused<2>(P, Pv, k - 1, SH, WH, hrho, hc, gamma0, g, gp, hy_new, hg, s_pend, hy_pend, d, hg);
-          else if (GM == 3) compact_products_fused<3>(P, Pv, k - 1, SH, WH, hrho, hc, gamma0, g, gp, hy_new, hg, s_pend, hy_pend, d, hg);
-          else if (GM == 4) compact_products_fused<4>(P, Pv, k - 1, SH, WH, hrho, hc, gamma0, g, gp, hy_new, hg, s_pend, hy_pend, d, hg);
+          if (GM <= 1) compact_products_fused<1>(P, Pv, k - 1, SH, WH, LH, lcap, hrho, hc, gamma0, g, gp, hy_new, hg, s_pend, hy_pend, d, hg);
+          else if (GM == 2) compact_products_fused<2>(P, Pv, k - 1, SH, WH, LH, lcap, hrho, hc, gamma0, g, gp, hy_new, hg, s_pend, hy_pend, d, hg);
+          else if (GM == 3) compact_products_fused<3>(P, Pv, k - 1, SH, WH, LH, lcap, hrho, hc, gamma0, g, gp, hy_new, hg, s_pend, hy_pend, d, hg);
+          else if (GM == 4) compact_products_fused<4>(P, Pv, k - 1, SH, WH, LH, lcap, hrho, hc, gamma0, g, gp, hy_new, hg, s_pend, hy_pend, d, hg);
           else
 #endif
           // GV mode (very long rows, few resident waves): 8 column groups in flight per lane;
@@ -647,6 +697,7 @@ __global__ __launch_bounds__(kWave * solve_waves(GV), DAVA_SOLVE_WAVES_PER_EU) v
         }
 #endif
         __syncthreads();
+        DAVA_PHASE(1);
         for (int i = tid; i < P; i += BLOCK) {
           const float gi = g[i], yi = gi - gp[i], si = s_cur[i], hi = hy_new[i];
           r[0] += si * yi; r[1] += hi * yi; r[2] += si * gi; r[3] += hi * gi;
@@ -670,10 +721,15 @@ __global__ __launch_bounds__(kWave * solve_waves(GV), DAVA_SOLVE_WAVES_PER_EU) v
         pend_rho = rho;
         pend_c = c;
       } else if (k - 1 < a.kcap) {
-        // append U_k = (s, H y, rho, c) to the history (entry k-1)
-        float* sr = SH + (size_t)(k - 1) * Pv;
-        float* wr = WH + (size_t)(k - 1) * Pv;
-        for (int i = tid; i < Pv; i += BLOCK) { sr[i] = s_cur[i]; wr[i] = hy_new[i]; }
+        // append U_k = (s, H y, rho, c) to the history (entry k-1), on-chip if it is one of the first lcap
+        if (k - 1 < lcap) {
+          float* sr = LH + (size_t)2 * (k - 1) * Pv;
+          for (int i = tid; i < Pv; i += BLOCK) { sr[i] = s_cur[i]; sr[Pv + i] = hy_new[i]; }
+        } else {
+          float* sr = SH + (size_t)(k - 1) * Pv;
+          float* wr = WH + (size_t)(k - 1) * Pv;
+          for (int i = tid; i < Pv; i += BLOCK) { sr[i] = s_cur[i]; wr[i] = hy_new[i]; }
+        }
         if (tid == 0) { hrho[k - 1] = rho; hc[k - 1] = c; }
       }
       __syncthreads();
@@ -687,6 +743,7 @@ __global__ __launch_bounds__(kWave * solve_waves(GV), DAVA_SOLVE_WAVES_PER_EU) v
       block_sum<1, NW>(r, scratch, buf); buf ^= 1;
       dphi0 = r[0];
     }
+    DAVA_PHASE(2);
     float a_lo = 0.f, a_hi = 0.f, al = 1.f, f_lo = E, f_hi = E, fa = E, dfa = dphi0;
     float last_al = 0.f, last_fa = 0.f;
     bool widen = true, zoom = false, evaluated = false, last_same = false;
@@ -698,6 +755,7 @@ __global__ __launch_bounds__(kWave * solve_waves(GV), DAVA_SOLVE_WAVES_PER_EU) v
         if (widen) { a_hi = al; f_hi = fa; al = 2.0f * al; }
         if (zoom) al = 0.5f * (a_lo + a_hi);
       }
+      DAVA_PHASE(4);
       // Trial points that round back to x exactly (tiny alpha, e.g. bisecting an uphill
       // direction at fp32 stagnation) need no evaluation: the reference's closure would
       // return f(x) and, via autograd w.r.t. alpha, (d * g).sum() -- exactly f0 and
@@ -713,6 +771,7 @@ __global__ __launch_bounds__(kWave * solve_waves(GV), DAVA_SOLVE_WAVES_PER_EU) v
         dfa = dphi0;
         last_same = true;
       }
+      DAVA_PHASE(3);
       ++trials;
       evaluated = true;
       last_al = al;
@@ -748,6 +807,7 @@ __global__ __launch_bounds__(kWave * solve_waves(GV), DAVA_SOLVE_WAVES_PER_EU) v
     if (have_next && last_same) {  // x_{k+1} == x_k bitwise: its gradient is g itself
       for (int i = tid; i < P; i += BLOCK) gp[i] = g[i];
     }
+    DAVA_PHASE(4);
 
     // ---- take the step (bfgs_solver.py:191-199) and test its length (:203-207) ----
     {
@@ -760,9 +820,15 @@ __global__ __launch_bounds__(kWave * solve_waves(GV), DAVA_SOLVE_WAVES_PER_EU) v
       }
       block_sum<1, NW>(r, scratch, buf); buf ^= 1;
       ++steps;
+      DAVA_PHASE(5);
       if (!(sqrtf(r[0]) > a.min_step)) { reason = DAVA_STOP_STEP; break; }
     }
   }
+#if DAVA_PHASE_TIMING
+  ph_acc[kPhases - 1] = clock64() - ph_start;
+  if (tid == 0 && a.phase_cycles)
+    for (int i = 0; i < kPhases; ++i) a.phase_cycles[(size_t)b * kPhases + i] = ph_acc[i];
+#endif
 
   // ---- outputs ----
   __syncthreads();
@@ -864,8 +930,9 @@ static size_t dense_hessian_bytes(const DavaScene* s) {
 #ifndef DAVA_EXTRA_LDS
 #define DAVA_EXTRA_LDS 0  // diagnostic builds only: pad LDS to force fewer workgroups per CU
 #endif
-static int lds_bytes_for(const DavaScene* s, int kcap = 0, bool gv = false) {
-  return carve_lds(s->num_views, s->num_points, round_up(s->num_parameters, 4), kcap, gv).total_bytes + DAVA_EXTRA_LDS;
+static int lds_bytes_for(const DavaScene* s, int kcap = 0, bool gv = false, int lcap = 0) {
+  return carve_lds(s->num_views, s->num_points, round_up(s->num_parameters, 4), kcap, gv, lcap).total_bytes +
+         DAVA_EXTRA_LDS;
 }
 
 // Global-vector mode when the all-in-LDS image would cost more than two workgroups
@@ -889,6 +956,25 @@ static size_t compact_history_bytes(const DavaScene* s, const DavaSolverConfig* 
 
 constexpr int kMaxLds = 160 * 1024;
 
+// COMPACT, LDS mode, single-pass products: how many of the oldest history entries to keep
+// on-chip.  Default: whatever fits beside the problem image without dropping below two
+// workgroups per CU (80 KiB each); DAVA_LDS_HISTORY=n overrides (A/B and tests; 0 = all in
+// HBM; values past one workgroup's LDS are clamped).
+constexpr int kLdsPerWorkgroupAt2 = 80 * 1024;
+static int lds_history_entries(const DavaScene* s, int kcap, bool gv) {
+#ifdef DAVA_COMPACT_TWO_PASS
+  return 0;
+#endif
+  const int Pv = round_up(s->num_parameters, 4);
+  if (gv || kcap <= 0 || (Pv / 4 + kWave - 1) / kWave > 4) return 0;
+  const int base = lds_bytes_for(s, kcap, false, 0);
+  const int per = 2 * Pv * (int)sizeof(float);
+  int n = (kLdsPerWorkgroupAt2 - base) / per;
+  if (const char* e = getenv("DAVA_LDS_HISTORY")) n = atoi(e);
+  n = min(n, (kMaxLds - base) / per);
+  return max(0, min(n, kcap));
+}
+
 }  // namespace dava
 
 using namespace dava;
@@ -900,6 +986,22 @@ extern "C" size_t dava_ba_solve_workspace_bytes(const DavaScene* scene, const Da
   if (config->hessian_mode == DAVA_HESSIAN_DENSE) return vec + dense_hessian_bytes(scene);
   if (config->hessian_mode == DAVA_HESSIAN_COMPACT) return vec + compact_history_bytes(scene, config);
   return 0;
+}
+
+extern "C" int dava_ba_solve_plan(const DavaScene* scene, const DavaSolverConfig* config, DavaSolvePlan* plan) {
+  const int st = check_scene(scene, false);
+  if (st != DAVA_OK) return st;
+  if (!config || !plan || config->iterations < 0) return DAVA_ERR_INVALID_ARGUMENT;
+  const int mode = config->hessian_mode;
+  if (mode != DAVA_HESSIAN_DENSE && mode != DAVA_HESSIAN_COMPACT) return DAVA_ERR_INVALID_ARGUMENT;
+  const int kcap = mode == DAVA_HESSIAN_COMPACT ? compact_capacity(config) : 0;
+  const bool gv = use_gv(scene, kcap);
+  const int lcap = mode == DAVA_HESSIAN_COMPACT ? lds_history_entries(scene, kcap, gv) : 0;
+  plan->global_vectors = gv ? 1 : 0;
+  plan->workgroup_threads = kWave * solve_waves(gv);
+  plan->lds_bytes = lds_bytes_for(scene, kcap, gv, lcap);
+  plan->lds_history_entries = lcap;
+  return plan->lds_bytes > kMaxLds || kcap > kMaxCompactEntries ? DAVA_ERR_UNSUPPORTED : DAVA_OK;
 }
 
 template <int MODE, bool GV, int RES>
@@ -929,7 +1031,8 @@ extern "C" int dava_ba_solve(const DavaScene* scene, const DavaSolverConfig* con
   const int kcap = mode == DAVA_HESSIAN_COMPACT ? compact_capacity(config) : 0;
   if (kcap > kMaxCompactEntries) return DAVA_ERR_UNSUPPORTED;
   const bool gv = use_gv(scene, kcap);
-  const int lds = lds_bytes_for(scene, kcap, gv);
+  const int lcap = mode == DAVA_HESSIAN_COMPACT ? lds_history_entries(scene, kcap, gv) : 0;
+  const int lds = lds_bytes_for(scene, kcap, gv, lcap);
   if (lds > kMaxLds) return DAVA_ERR_UNSUPPORTED;
   const size_t vec = gv ? gv_vector_bytes(scene) : 0;
   const size_t need = vec + (mode == DAVA_HESSIAN_DENSE ? dense_hessian_bytes(scene) : compact_history_bytes(scene, config));
@@ -957,7 +1060,14 @@ extern "C" int dava_ba_solve(const DavaScene* scene, const DavaSolverConfig* con
   a.strong = config->strong_wolfe;
   a.mode = mode;
   a.kcap = kcap;
+  a.lcap = lcap;
+  a.phase_cycles = nullptr;
   hipStream_t s = static_cast<hipStream_t>(stream);
+#if DAVA_PHASE_TIMING
+  const size_t ph_bytes = (size_t)scene->batch * kPhases * sizeof(unsigned long long);
+  if (hipMalloc(&a.phase_cycles, ph_bytes) != hipSuccess) return DAVA_ERR_LAUNCH;
+  (void)hipMemsetAsync(a.phase_cycles, 0, ph_bytes, s);
+#endif
   if (mode == DAVA_HESSIAN_DENSE) {
     if (gv) launch_solve<DAVA_HESSIAN_DENSE, true>(a, scene->batch, lds, s, scene->residual);
     else launch_solve<DAVA_HESSIAN_DENSE, false>(a, scene->batch, lds, s, scene->residual);
@@ -965,7 +1075,25 @@ extern "C" int dava_ba_solve(const DavaScene* scene, const DavaSolverConfig* con
     if (gv) launch_solve<DAVA_HESSIAN_COMPACT, true>(a, scene->batch, lds, s, scene->residual);
     else launch_solve<DAVA_HESSIAN_COMPACT, false>(a, scene->batch, lds, s, scene->residual);
   }
-  return hipGetLastError() == hipSuccess ? DAVA_OK : DAVA_ERR_LAUNCH;
+  const bool launched = hipGetLastError() == hipSuccess;
+#if DAVA_PHASE_TIMING
+  {
+    unsigned long long* h = static_cast<unsigned long long*>(malloc(ph_bytes));
+    (void)hipStreamSynchronize(s);
+    (void)hipMemcpy(h, a.phase_cycles, ph_bytes, hipMemcpyDeviceToHost);
+    (void)hipFree(a.phase_cycles);
+    static const char* names[kPhases] = {"eval_at_x", "history", "direction", "trial_evals", "search_logic", "step",
+                                         "total"};
+    double avg[kPhases] = {0};
+    for (int b = 0; b < scene->batch; ++b)
+      for (int i = 0; i < kPhases; ++i) avg[i] += (double)h[(size_t)b * kPhases + i] / scene->batch;
+    fprintf(stderr, "[dava phase cycles / problem]");
+    for (int i = 0; i < kPhases; ++i) fprintf(stderr, " %s=%.0f (%.1f%%)", names[i], avg[i], 100.0 * avg[i] / avg[kPhases - 1]);
+    fprintf(stderr, "\n");
+    free(h);
+  }
+#endif
+  return launched ? DAVA_OK : DAVA_ERR_LAUNCH;
 }
 
 template <bool G, bool S, bool T, bool GV, int RES>

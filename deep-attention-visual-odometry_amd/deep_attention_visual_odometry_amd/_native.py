@@ -55,9 +55,20 @@ class DavaSolverConfig(ctypes.Structure):
     ]
 
 
+class DavaSolvePlan(ctypes.Structure):
+    _fields_ = [
+        ("global_vectors", _c_i32),
+        ("workgroup_threads", _c_i32),
+        ("lds_bytes", _c_i32),
+        ("lds_history_entries", _c_i32),
+    ]
+
+
 # name -> (restype, argtypes); every symbol declared in include/dava_ba.h
 SIGNATURES = {
     "dava_ba_solve_workspace_bytes": (ctypes.c_size_t, [ctypes.POINTER(DavaScene), ctypes.POINTER(DavaSolverConfig)]),
+    "dava_ba_solve_plan": (ctypes.c_int, [ctypes.POINTER(DavaScene), ctypes.POINTER(DavaSolverConfig),
+                                          ctypes.POINTER(DavaSolvePlan)]),
     "dava_ba_solve": (ctypes.c_int, [ctypes.POINTER(DavaScene), ctypes.POINTER(DavaSolverConfig), _vp, _vp, _vp, _vp,
                                      _vp, ctypes.c_size_t, _vp]),
     "dava_ba_evaluate": (ctypes.c_int, [ctypes.POINTER(DavaScene), _vp, _vp, _vp, _vp, _vp, _vp, _vp]),

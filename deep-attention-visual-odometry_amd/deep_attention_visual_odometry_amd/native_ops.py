@@ -122,6 +122,19 @@ def solve_workspace_bytes(batch: int, num_views: int, num_points: int, distortio
     return int(lib.dava_ba_solve_workspace_bytes(sc, cfg))
 
 
+def solve_plan(batch: int, num_views: int, num_points: int, distortion: bool,
+               hessian_mode: int = N.DAVA_HESSIAN_DENSE, iterations: int = 1000,
+               residual: int = N.DAVA_RESIDUAL_SQUARED_REPROJECTION) -> dict:
+    """How ``dava_ba_solve`` runs this shape (host-only query): global-vector mode, workgroup
+    size, LDS bytes and the number of history entries kept on-chip (COMPACT)."""
+    lib = N.load_library()
+    sc = scene_struct(None, None, num_views, num_points, distortion, batch, residual)
+    cfg = N.DavaSolverConfig(1e-4, 0.9, 1e-4, 1e-8, iterations, 1000, 1, hessian_mode)
+    plan = N.DavaSolvePlan()
+    N.check(lib.dava_ba_solve_plan(sc, cfg, plan), "dava_ba_solve_plan")
+    return {name: int(getattr(plan, name)) for name, _ in N.DavaSolvePlan._fields_}
+
+
 # ---- generic BFGS building blocks ----
 # Each public op is a torch.autograd.Function whose forward AND backward are HIP kernels
 # (bfgs_ops.hip / bfgs_grad.hip), so the drop-in solver can be differentiated through

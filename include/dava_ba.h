@@ -103,6 +103,16 @@ typedef struct DavaSolverConfig {
 /* Bytes of device workspace dava_ba_solve needs for this scene/config. */
 size_t dava_ba_solve_workspace_bytes(const DavaScene* scene, const DavaSolverConfig* config);
 
+/* How dava_ba_solve runs a scene/config (host-only query, no device needed): lets a caller
+ * account for the HBM traffic of the launch (benchmarks, roofline) without re-deriving it. */
+typedef struct DavaSolvePlan {
+  int32_t global_vectors;      /* 1: the O(P) state lives in the workspace (large P), 0: in LDS  */
+  int32_t workgroup_threads;   /* threads of the one workgroup that solves a problem            */
+  int32_t lds_bytes;           /* dynamic LDS per workgroup                                     */
+  int32_t lds_history_entries; /* COMPACT: the oldest history entries kept on-chip, never in HBM */
+} DavaSolvePlan;
+int dava_ba_solve_plan(const DavaScene* scene, const DavaSolverConfig* config, DavaSolvePlan* plan_out);
+
 /* The whole eval-mode solve, one launch.
  * Replaces BFGSSolver.forward(parameters, error_function)
  * (autograd_solvers/bfgs_solver.py:80-215) with error_function = the objective

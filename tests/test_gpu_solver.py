@@ -229,6 +229,26 @@ def test_global_vector_mode_equals_lds_mode(device, mode, monkeypatch):
     assert _rel(gv, lds).max() <= TOL
 
 
+@pytest.mark.parametrize("m,n,distortion", [(4, 256, True), (2, 128, False)])
+def test_lds_resident_history_is_bitwise_invisible(device, m, n, distortion, monkeypatch):
+    """COMPACT mode keeps the oldest history entries on-chip (dava_ba_solve_plan); the products
+    read the same values in the same order, so the result must not change by a single bit
+    whether 0, the default or (past two workgroups per CU) 18 entries stay in LDS."""
+    from deep_attention_visual_odometry_amd import native_ops
+
+    x0, obs, vis = _scene(16, m, n, distortion, 558)
+    kw = dict(iterations=40, error_threshold=-1.0, minimum_step=-1.0, hessian_mode="compact")
+    assert native_ops.solve_plan(16, m, n, distortion, 1, 40)["lds_history_entries"] > 0
+    ref, st_ref = _gpu_solve(device, x0, obs, vis, m, n, distortion, **kw)
+    for entries in ("0", "18"):
+        monkeypatch.setenv("DAVA_LDS_HISTORY", entries)
+        assert native_ops.solve_plan(16, m, n, distortion, 1, 40)["lds_history_entries"] == int(entries)
+        out, st = _gpu_solve(device, x0, obs, vis, m, n, distortion, **kw)
+        assert torch.equal(out, ref), entries
+        assert torch.equal(st, st_ref), entries
+    monkeypatch.delenv("DAVA_LDS_HISTORY")
+
+
 # ---- ray-angle residual (CalibrationNetwork's error, calibration_network.py:58-67) ----
 
 def _gpu_solve_ray(device, x0, obs, vis, m, n, **kw):

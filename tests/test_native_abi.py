@@ -82,6 +82,23 @@ def test_workspace_size_dense(lib):
     assert native_ops.solve_workspace_bytes(8192, 4, 256, True) == 8192 * p * ((p + 31) // 32 * 32) * 4
 
 
+def test_solve_plan(lib, monkeypatch):
+    """Host-only plan query: C3 keeps its oldest history entries in LDS within two workgroups
+    per CU; C5 (P = 12381) runs the O(P) state from HBM in 512-thread workgroups."""
+    from deep_attention_visual_odometry_amd import native_ops
+
+    monkeypatch.delenv("DAVA_LDS_HISTORY", raising=False)
+    c3 = native_ops.solve_plan(8192, 4, 256, True, 1, 100)
+    assert c3["global_vectors"] == 0 and c3["workgroup_threads"] == 256
+    assert c3["lds_history_entries"] > 0 and c3["lds_bytes"] <= 80 * 1024
+    assert native_ops.solve_plan(8192, 4, 256, True, 0, 100)["lds_history_entries"] == 0  # dense
+    c5 = native_ops.solve_plan(256, 16, 4096, False, 1, 100)
+    assert c5["global_vectors"] == 1 and c5["workgroup_threads"] == 512 and c5["lds_history_entries"] == 0
+    monkeypatch.setenv("DAVA_LDS_HISTORY", "1000")  # clamped to one workgroup's LDS
+    big = native_ops.solve_plan(8192, 4, 256, True, 1, 100)
+    assert big["lds_bytes"] <= 160 * 1024 and big["lds_history_entries"] > c3["lds_history_entries"]
+
+
 def test_product_refuses_cpu_tensors():
     import torch
 
