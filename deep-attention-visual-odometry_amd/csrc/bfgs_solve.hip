@@ -48,7 +48,7 @@ struct SolveArgs {
 };
 
 struct LdsCarve {
-  int x, d, g0, g1, s0, s1, hy0, hy1, hg, obs, views, vpart, scratch, hcoef, hrho, hc, hist, vis_bytes_off,
+  int x, d, ge, g0, g1, s0, s1, hy0, hy1, hg, obs, views, vpart, scratch, hcoef, hrho, hc, hist, vis_bytes_off,
       total_bytes;
 };
 
@@ -75,13 +75,22 @@ __host__ __device__ inline bool wide_history_pass(int Pv, int kcap, bool gv) {
 // COMPACT LDS mode may keep the OLDEST lcap history entries on-chip (S row then W row,
 // 2 Pv floats per entry): entry j is read by every iteration k > j + 1, so the first
 // entries carry the most traffic (lcap = 6 at C3 removes 12% of the history reads).
-__host__ __device__ inline LdsCarve carve_lds(int M, int N, int Pv, int kcap = 0, bool gv = false, int lcap = 0) {
+// GV mode with xl ("x local"): x, d and the objective's gradient output (ge) still fit in
+// LDS (3 Pv floats; C5: 149 KB), so the objective -- whose per-(view, point) work reads x
+// and d and accumulates point gradients view after view, one dependent access per pair --
+// runs on-chip; the other vectors stay in the workspace slice (its x and d slots unused).
+__host__ __device__ inline LdsCarve carve_lds(int M, int N, int Pv, int kcap = 0, bool gv = false, int lcap = 0,
+                                              bool xl = false) {
   LdsCarve c;
   int off = 0;
   int voff = 0;
   int& o = gv ? voff : off;
-  c.x = o; o += Pv;
-  c.d = o; o += Pv;
+  int& ox = gv && !xl ? voff : off;
+  c.x = ox; ox += Pv;
+  c.d = ox; ox += Pv;
+  if (gv && xl) voff += 2 * Pv;
+  c.ge = gv && xl ? off : 0;
+  off += gv && xl ? Pv : 0;
   c.g0 = o; o += Pv;
   c.g1 = o; o += Pv;
   c.s0 = o; o += Pv;
@@ -549,8 +558,9 @@ __device__ __forceinline__ void compact_products_fused(int P, int Pv, int nh, co
   }
 }
 
-template <int MODE, bool GV, int RES>
+template <int MODE, bool GV, int RES, bool XL>  // XL: GV mode with x, d and the objective's gradient in LDS
 __global__ __launch_bounds__(kWave * solve_waves(GV), DAVA_SOLVE_WAVES_PER_EU) void bfgs_ba_solve_kernel(SolveArgs a) {
+  static_assert(!XL || GV, "XL is a global-vector-mode variant");
   constexpr int NW = solve_waves(GV);
   constexpr int BLOCK = kWave * NW;
   extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -560,11 +570,20 @@ __global__ __launch_bounds__(kWave * solve_waves(GV), DAVA_SOLVE_WAVES_PER_EU) v
   const int b = blockIdx.x;
   const int tid = threadIdx.x;
   const int lcap = MODE == DAVA_HESSIAN_COMPACT && !GV ? a.lcap : 0;
-  const LdsCarve cv = carve_lds(M, N, Pv, MODE == DAVA_HESSIAN_COMPACT ? a.kcap : 0, GV, lcap);
+  const LdsCarve cv = carve_lds(M, N, Pv, MODE == DAVA_HESSIAN_COMPACT ? a.kcap : 0, GV, lcap, XL);
   float* LH = lds + cv.hist;  // LDS-resident history entries 0 .. lcap-1
   float* vb0 = GV ? a.vecs + (size_t)b * kVectors * Pv : lds;
-  float* x = vb0 + cv.x;
-  float* d = vb0 + cv.d;
+  float* x = (GV && !XL ? vb0 : lds) + cv.x;
+  float* d = (GV && !XL ? vb0 : lds) + cv.d;
+  float* ge = lds + cv.ge;  // XL: the objective's gradient output, copied to g / gp after each evaluation
+  // the objective's gradient target and its publication to the workspace vector `dst`
+  auto grad_buf = [&](float* dst) { return XL ? ge : dst; };
+  auto publish = [&](float* dst) {
+    if constexpr (XL) {
+      for (int i = tid; i < P; i += BLOCK) dst[i] = ge[i];
+      __syncthreads();
+    }
+  };
   float* g = vb0 + cv.g0;
   float* gp = vb0 + cv.g1;
   float* hcoef = lds + cv.hcoef;
@@ -628,8 +647,9 @@ __global__ __launch_bounds__(kWave * solve_waves(GV), DAVA_SOLVE_WAVES_PER_EU) v
     if (have_next) {
       E = E_next;
     } else {
-      ba_eval<true, false, false, false, false, RES, float, NW>(L, x, nullptr, 0.f, obs, vis, g, views, vpart, scratch, buf, E,
-                                                     unused);
+      ba_eval<true, false, false, false, false, RES, float, NW>(L, x, nullptr, 0.f, obs, vis, grad_buf(g), views, vpart,
+                                                                scratch, buf, E, unused);
+      publish(g);
       ++evals;
     }
     DAVA_PHASE(0);
@@ -746,6 +766,12 @@ __global__ __launch_bounds__(kWave * solve_waves(GV), DAVA_SOLVE_WAVES_PER_EU) v
     DAVA_PHASE(2);
     float a_lo = 0.f, a_hi = 0.f, al = 1.f, f_lo = E, f_hi = E, fa = E, dfa = dphi0;
     float last_al = 0.f, last_fa = 0.f;
+    // Largest alpha seen whose trial point rounded back to x.  Rounding is monotone
+    // (0 <= a' <= a => |fl(a' d_i)| <= |fl(a d_i)| and fl(x_i + .) stays x_i), so every smaller
+    // trial is a no-move point too and needs neither evaluation nor the check: at fp32
+    // stagnation a bisection towards 0 runs ~150 such trials per line search (C2's slowest
+    // problems: thousands per solve).
+    float nomove_al = -1.0f;
     bool widen = true, zoom = false, evaluated = false, last_same = false;
     // trial gradients go into gp's buffer (g_prev is dead once d is formed)
     const float lim = (-a.c2) * dphi0;
@@ -762,14 +788,17 @@ __global__ __launch_bounds__(kWave * solve_waves(GV), DAVA_SOLVE_WAVES_PER_EU) v
       // phi'(0).  The check rides on the objective's first reduction (CHECK).  Otherwise
       // E and the full gradient at the trial point are formed (kept for reuse as the
       // next iterate's gradient) and phi'(alpha) = d . grad (DOT).
-      if (ba_eval<true, !DAVA_TRIAL_DOT, true, DAVA_TRIAL_DOT, DAVA_TRIAL_CHECK, RES, float, NW>(L, x, d, al, obs, vis, gp, views, vpart,
-                                                                     scratch, buf, fa, dfa)) {
+      const bool known_same = DAVA_TRIAL_CHECK && al <= nomove_al;  // uniform
+      if (!known_same &&
+          ba_eval<true, !DAVA_TRIAL_DOT, true, DAVA_TRIAL_DOT, DAVA_TRIAL_CHECK, RES, float, NW>(
+              L, x, d, al, obs, vis, grad_buf(gp), views, vpart, scratch, buf, fa, dfa)) {
         ++evals;
         last_same = false;
       } else {
         fa = E;
         dfa = dphi0;
         last_same = true;
+        if (!known_same) nomove_al = al;
       }
       DAVA_PHASE(3);
       ++trials;
@@ -806,6 +835,8 @@ __global__ __launch_bounds__(kWave * solve_waves(GV), DAVA_SOLVE_WAVES_PER_EU) v
     E_next = last_fa;
     if (have_next && last_same) {  // x_{k+1} == x_k bitwise: its gradient is g itself
       for (int i = tid; i < P; i += BLOCK) gp[i] = g[i];
+    } else if (have_next) {
+      publish(gp);  // XL: only the trial that is kept needs its gradient in the workspace
     }
     DAVA_PHASE(4);
 
@@ -930,17 +961,24 @@ static size_t dense_hessian_bytes(const DavaScene* s) {
 #ifndef DAVA_EXTRA_LDS
 #define DAVA_EXTRA_LDS 0  // diagnostic builds only: pad LDS to force fewer workgroups per CU
 #endif
-static int lds_bytes_for(const DavaScene* s, int kcap = 0, bool gv = false, int lcap = 0) {
-  return carve_lds(s->num_views, s->num_points, round_up(s->num_parameters, 4), kcap, gv, lcap).total_bytes +
+static int lds_bytes_for(const DavaScene* s, int kcap = 0, bool gv = false, int lcap = 0, bool xl = false) {
+  return carve_lds(s->num_views, s->num_points, round_up(s->num_parameters, 4), kcap, gv, lcap, xl).total_bytes +
          DAVA_EXTRA_LDS;
 }
 
 // Global-vector mode when the all-in-LDS image would cost more than two workgroups
 // per CU (e.g. C5: P = 12381 -> 446 KB of vectors per problem).
 constexpr int kLdsModeBudget = 72 * 1024;
+constexpr int kMaxLds = 160 * 1024;
 static bool use_gv(const DavaScene* s, int kcap = 0) {
   const bool force = getenv("DAVA_FORCE_GV") != nullptr;  // test knob: cross-check GV vs LDS mode
   return force || lds_bytes_for(s, kcap, false) > kLdsModeBudget;
+}
+// GV mode: run the objective on LDS copies of x and d (carve_lds `xl`) whenever they fit
+// beside the rest of the image.  DAVA_GV_NO_XL forces the in-workspace variant (tests).
+static bool use_xl(const DavaScene* s, int kcap, bool gv) {
+  if (!gv || getenv("DAVA_GV_NO_XL") != nullptr) return false;
+  return lds_bytes_for(s, kcap, true, 0, true) <= kMaxLds;
 }
 static size_t gv_vector_bytes(const DavaScene* s) {
   return (size_t)s->batch * kVectors * (size_t)round_up(s->num_parameters, 4) * sizeof(float);
@@ -953,8 +991,6 @@ constexpr int kMaxCompactEntries = 1024;
 static size_t compact_history_bytes(const DavaScene* s, const DavaSolverConfig* c) {
   return (size_t)s->batch * 2 * (size_t)compact_capacity(c) * (size_t)round_up(s->num_parameters, 4) * sizeof(float);
 }
-
-constexpr int kMaxLds = 160 * 1024;
 
 // COMPACT, LDS mode, single-pass products: how many of the oldest history entries to keep
 // on-chip.  Default: whatever fits beside the problem image without dropping below two
@@ -999,23 +1035,23 @@ extern "C" int dava_ba_solve_plan(const DavaScene* scene, const DavaSolverConfig
   const int lcap = mode == DAVA_HESSIAN_COMPACT ? lds_history_entries(scene, kcap, gv) : 0;
   plan->global_vectors = gv ? 1 : 0;
   plan->workgroup_threads = kWave * solve_waves(gv);
-  plan->lds_bytes = lds_bytes_for(scene, kcap, gv, lcap);
+  plan->lds_bytes = lds_bytes_for(scene, kcap, gv, lcap, use_xl(scene, kcap, gv));
   plan->lds_history_entries = lcap;
   return plan->lds_bytes > kMaxLds || kcap > kMaxCompactEntries ? DAVA_ERR_UNSUPPORTED : DAVA_OK;
 }
 
-template <int MODE, bool GV, int RES>
+template <int MODE, bool GV, int RES, bool XL>
 static void launch_solve_res(const SolveArgs& a, int B, int lds, hipStream_t s) {
   if (lds > 64 * 1024)
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(bfgs_ba_solve_kernel<MODE, GV, RES>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(bfgs_ba_solve_kernel<MODE, GV, RES, XL>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-  hipLaunchKernelGGL((bfgs_ba_solve_kernel<MODE, GV, RES>), dim3(B), dim3(kWave * solve_waves(GV)), lds, s, a);
+  hipLaunchKernelGGL((bfgs_ba_solve_kernel<MODE, GV, RES, XL>), dim3(B), dim3(kWave * solve_waves(GV)), lds, s, a);
 }
 
-template <int MODE, bool GV>
+template <int MODE, bool GV, bool XL = false>
 static void launch_solve(const SolveArgs& a, int B, int lds, hipStream_t s, int residual) {
-  if (residual == DAVA_RESIDUAL_RAY_ANGLE) launch_solve_res<MODE, GV, DAVA_RESIDUAL_RAY_ANGLE>(a, B, lds, s);
-  else launch_solve_res<MODE, GV, DAVA_RESIDUAL_SQUARED_REPROJECTION>(a, B, lds, s);
+  if (residual == DAVA_RESIDUAL_RAY_ANGLE) launch_solve_res<MODE, GV, DAVA_RESIDUAL_RAY_ANGLE, XL>(a, B, lds, s);
+  else launch_solve_res<MODE, GV, DAVA_RESIDUAL_SQUARED_REPROJECTION, XL>(a, B, lds, s);
 }
 
 extern "C" int dava_ba_solve(const DavaScene* scene, const DavaSolverConfig* config, const float* x0,
@@ -1031,8 +1067,9 @@ extern "C" int dava_ba_solve(const DavaScene* scene, const DavaSolverConfig* con
   const int kcap = mode == DAVA_HESSIAN_COMPACT ? compact_capacity(config) : 0;
   if (kcap > kMaxCompactEntries) return DAVA_ERR_UNSUPPORTED;
   const bool gv = use_gv(scene, kcap);
+  const bool xl = use_xl(scene, kcap, gv);
   const int lcap = mode == DAVA_HESSIAN_COMPACT ? lds_history_entries(scene, kcap, gv) : 0;
-  const int lds = lds_bytes_for(scene, kcap, gv, lcap);
+  const int lds = lds_bytes_for(scene, kcap, gv, lcap, xl);
   if (lds > kMaxLds) return DAVA_ERR_UNSUPPORTED;
   const size_t vec = gv ? gv_vector_bytes(scene) : 0;
   const size_t need = vec + (mode == DAVA_HESSIAN_DENSE ? dense_hessian_bytes(scene) : compact_history_bytes(scene, config));
@@ -1069,10 +1106,12 @@ extern "C" int dava_ba_solve(const DavaScene* scene, const DavaSolverConfig* con
   (void)hipMemsetAsync(a.phase_cycles, 0, ph_bytes, s);
 #endif
   if (mode == DAVA_HESSIAN_DENSE) {
-    if (gv) launch_solve<DAVA_HESSIAN_DENSE, true>(a, scene->batch, lds, s, scene->residual);
+    if (xl) launch_solve<DAVA_HESSIAN_DENSE, true, true>(a, scene->batch, lds, s, scene->residual);
+    else if (gv) launch_solve<DAVA_HESSIAN_DENSE, true>(a, scene->batch, lds, s, scene->residual);
     else launch_solve<DAVA_HESSIAN_DENSE, false>(a, scene->batch, lds, s, scene->residual);
   } else {
-    if (gv) launch_solve<DAVA_HESSIAN_COMPACT, true>(a, scene->batch, lds, s, scene->residual);
+    if (xl) launch_solve<DAVA_HESSIAN_COMPACT, true, true>(a, scene->batch, lds, s, scene->residual);
+    else if (gv) launch_solve<DAVA_HESSIAN_COMPACT, true>(a, scene->batch, lds, s, scene->residual);
     else launch_solve<DAVA_HESSIAN_COMPACT, false>(a, scene->batch, lds, s, scene->residual);
   }
   const bool launched = hipGetLastError() == hipSuccess;

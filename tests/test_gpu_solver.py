@@ -216,16 +216,21 @@ def test_c5_shape_objective_matches_oracle(device):
     assert torch.allclose(sl.cpu().double(), sl_ref, rtol=1e-3, atol=1e-6 * g_ref.norm().item())
 
 
+@pytest.mark.parametrize("xl", [True, False])
 @pytest.mark.parametrize("mode", ["dense", "compact"])
-def test_global_vector_mode_equals_lds_mode(device, mode, monkeypatch):
+def test_global_vector_mode_equals_lds_mode(device, mode, xl, monkeypatch):
     """The same C3-shaped solve with the O(P) state forced into HBM (DAVA_FORCE_GV) agrees with
-    the LDS-resident kernel (same device code, different memory)."""
+    the LDS-resident kernel (same device code, different memory), with the objective on LDS
+    copies of x and d (the default where they fit) or on the workspace vectors (DAVA_GV_NO_XL)."""
     x0, obs, vis = _scene(8, 4, 256, True, 557)
     kw = dict(iterations=30, error_threshold=-1.0, minimum_step=-1.0, hessian_mode=mode)
     lds, _ = _gpu_solve(device, x0, obs, vis, 4, 256, True, **kw)
     monkeypatch.setenv("DAVA_FORCE_GV", "1")
+    if not xl:
+        monkeypatch.setenv("DAVA_GV_NO_XL", "1")
     gv, _ = _gpu_solve(device, x0, obs, vis, 4, 256, True, **kw)
     monkeypatch.delenv("DAVA_FORCE_GV")
+    monkeypatch.delenv("DAVA_GV_NO_XL", raising=False)
     assert _rel(gv, lds).max() <= TOL
 
 
