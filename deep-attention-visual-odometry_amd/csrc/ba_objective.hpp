@@ -173,14 +173,19 @@ __device__ __forceinline__ void ray_angle_pair(const RayAngle<S>& ra, const floa
 // CHECK (with TRIAL): if x + alpha d rounds to x in every component, return false right
 //        after the first reduction without evaluating (the caller knows the answer:
 //        f(x) and phi'(0)); otherwise evaluate and return true.
+// PPT > 0: every thread keeps its (at most PPT) points' trial coordinates, directions and
+//        gradients in registers for the whole view sweep (requires N <= PPT * threads);
+//        PPT = 0: they are re-read from / accumulated into x, d, grad view after view.
 template <bool GRAD, bool SLOPE, bool TRIAL, bool DOT = false, bool CHECK = false,
-          int RES = DAVA_RESIDUAL_SQUARED_REPROJECTION, typename S = float, int NW = kWaves>
+          int RES = DAVA_RESIDUAL_SQUARED_REPROJECTION, typename S = float, int NW = kWaves, int PPT = 0>
 __device__ __forceinline__ bool ba_eval(const Layout& L, const S* x, const S* d, float alpha, const float* obs,
                                         const uint8_t* vis, S* grad, S* views, S* vpart, float* scratch, int& buf,
                                         S& E_out, S& slope_out, S* obs_grad = nullptr) {
   constexpr int BLOCK = kWave * NW;  // threads in the workgroup
   static_assert(!DOT || (GRAD && !SLOPE), "DOT derives the slope from the reverse-mode gradient");
   static_assert(!CHECK || TRIAL, "CHECK needs a trial point");
+  constexpr int PR = PPT > 0 ? PPT : 1;
+  S Xr[PR][3], Dr[PR][3], Gr[PR][3];  // PPT > 0: this thread's points (n = tid + u BLOCK)
   const int tid = threadIdx.x;
   const int lane = tid & (kWave - 1);
   const int wave = tid / kWave;
@@ -215,14 +220,23 @@ __device__ __forceinline__ bool ba_eval(const Layout& L, const S* x, const S* d,
   // 2. scale normalisation s = (mean|X| N + mean|t| M)/(N+M), and its slope
   S sums[3] = {0.f, 0.f, 0.f};  // sum|X|, sum sgn(X) dX (SLOPE or DOT), moved (CHECK)
   bool moved = false;
-  for (int n = tid; n < N; n += BLOCK) {
+  auto point_sums = [&](int n, S (&Xp)[3], S (&Dp)[3]) {
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
       const S X = trial_value<TRIAL>(x, d, alpha, L.pt(n) + c);
+      Xp[c] = X;
+      Dp[c] = (SLOPE || DOT) ? d[L.pt(n) + c] : S(0.0f);
       sums[0] += fabs_(X);
-      if constexpr (SLOPE || DOT) sums[1] += sgn(X) * d[L.pt(n) + c];
+      if constexpr (SLOPE || DOT) sums[1] += sgn(X) * Dp[c];
       if constexpr (CHECK) moved |= X != x[L.pt(n) + c];
     }
+  };
+  if constexpr (PPT > 0) {
+#pragma unroll
+    for (int u = 0; u < PPT; ++u)
+      if (tid + u * BLOCK < N) point_sums(tid + u * BLOCK, Xr[u], Dr[u]);
+  } else {
+    for (int n = tid; n < N; n += BLOCK) point_sums(n, Xr[0], Dr[0]);
   }
   if constexpr (CHECK) {
     // the parameters that are not point coordinates: intrinsics, views, distortion
@@ -312,17 +326,19 @@ __device__ __forceinline__ bool ba_eval(const Layout& L, const S* x, const S* d,
     }
     S vg[7] = {0, 0, 0, 0, 0, 0, 0};  // gw_direct xyz, g_theta, g_t~ xyz
 
-    for (int n = tid; n < N; n += BLOCK) {
-      const int ip = L.pt(n);
-      const S X0 = trial_value<TRIAL>(x, d, alpha, ip + 0);
-      const S X1 = trial_value<TRIAL>(x, d, alpha, ip + 1);
-      const S X2 = trial_value<TRIAL>(x, d, alpha, ip + 2);
+    // one (view m, point n) pair.  X / dX: the point's trial coordinates and direction;
+    // q: its gradient, accumulated view after view (registers when PPT > 0, else loaded from
+    // and stored back to `grad` by the caller below -- the same additions in the same order)
+    auto pair = [&](int n, const S X0, const S X1, const S X2, const S dX0, const S dX1, const S dX2, S& q0, S& q1,
+                    S& q2) {
+      const float ob[2] = {obs[2 * (m * N + n)], obs[2 * (m * N + n) + 1]};
+      const uint8_t visible = vis[m * N + n];
       const S a0 = X0 * inv_s, a1 = X1 * inv_s, a2 = X2 * inv_s;  // X~ = X / s
       S da0 = 0.f, da1 = 0.f, da2 = 0.f;
       if constexpr (SLOPE) {
-        da0 = (d[ip + 0] - a0 * (ds_over_s * s)) * inv_s;
-        da1 = (d[ip + 1] - a1 * (ds_over_s * s)) * inv_s;
-        da2 = (d[ip + 2] - a2 * (ds_over_s * s)) * inv_s;
+        da0 = (dX0 - a0 * (ds_over_s * s)) * inv_s;
+        da1 = (dX1 - a1 * (ds_over_s * s)) * inv_s;
+        da2 = (dX2 - a2 * (ds_over_s * s)) * inv_s;
       }
       // camera-relative point p (and dp)
       S p0, p1, p2, dp0 = 0.f, dp1 = 0.f, dp2 = 0.f;
@@ -379,9 +395,8 @@ __device__ __forceinline__ bool ba_eval(const Layout& L, const S* x, const S* d,
           u = ub + in.cx;
           vv = vb + in.cy;
         }
-        const int pair = m * N + n;
-        const float wgt = vis[pair] ? 1.0f : 0.0f;
-        const S ru = u - obs[2 * pair], rv = vv - obs[2 * pair + 1];
+        const float wgt = visible ? 1.0f : 0.0f;
+        const S ru = u - ob[0], rv = vv - ob[1];
         e_loc += (ru * ru + rv * rv) * wgt;
         if constexpr (SLOPE) {
           S du = Juu * dub + Juv * dvb + din.cx;
@@ -418,8 +433,8 @@ __device__ __forceinline__ bool ba_eval(const Layout& L, const S* x, const S* d,
           G0 = gub * fi; G1 = gvb * fi; G2 = -(gub * ub + gvb * vb) * iz;
         }
       } else {
-        ray_angle_pair<GRAD, SLOPE, S>(ra, obs + 2 * (m * N + n), vis[m * N + n], p0, p1, p2, dp0, dp1, dp2,
-                                    e_loc, sl_loc, gin, G0, G1, G2, go0, go1);
+        ray_angle_pair<GRAD, SLOPE, S>(ra, ob, visible, p0, p1, p2, dp0, dp1, dp2, e_loc, sl_loc, gin, G0, G1, G2,
+                                       go0, go1);
       }
       if constexpr (GRAD && !std::is_same<S, float>::value) {
         if (obs_grad) {
@@ -448,13 +463,33 @@ __device__ __forceinline__ bool ba_eval(const Layout& L, const S* x, const S* d,
           vg[3] += -vs * Gv + vAp * vw * Gw + vTC * Gx;  // dE/dth
           vg[4] += G0; vg[5] += G1; vg[6] += G2;          // dE/dt~
         }
-        S* gp = grad + ip;
-        if (m == 0) { gp[0] = gx0; gp[1] = gx1; gp[2] = gx2; }
-        else { gp[0] += gx0; gp[1] += gx1; gp[2] += gx2; }
+        if (m == 0) { q0 = gx0; q1 = gx1; q2 = gx2; }
+        else { q0 += gx0; q1 += gx1; q2 += gx2; }
         if (m == M - 1) {
-          gsx += gp[0] * X0 + gp[1] * X1 + gp[2] * X2;
-          if constexpr (DOT) gdx += gp[0] * d[ip] + gp[1] * d[ip + 1] + gp[2] * d[ip + 2];
+          gsx += q0 * X0 + q1 * X1 + q2 * X2;
+          if constexpr (DOT) gdx += q0 * dX0 + q1 * dX1 + q2 * dX2;
         }
+      }
+    };
+    if constexpr (PPT > 0) {
+#pragma unroll
+      for (int u = 0; u < PPT; ++u) {
+        const int n = tid + u * BLOCK;
+        if (n < N) pair(n, Xr[u][0], Xr[u][1], Xr[u][2], Dr[u][0], Dr[u][1], Dr[u][2], Gr[u][0], Gr[u][1], Gr[u][2]);
+      }
+    } else {
+      for (int n = tid; n < N; n += BLOCK) {
+        const int ip = L.pt(n);
+        const S X0 = trial_value<TRIAL>(x, d, alpha, ip + 0);
+        const S X1 = trial_value<TRIAL>(x, d, alpha, ip + 1);
+        const S X2 = trial_value<TRIAL>(x, d, alpha, ip + 2);
+        S dX0 = 0.f, dX1 = 0.f, dX2 = 0.f, q0 = 0.f, q1 = 0.f, q2 = 0.f;
+        if constexpr (SLOPE || DOT) { dX0 = d[ip]; dX1 = d[ip + 1]; dX2 = d[ip + 2]; }
+        if constexpr (GRAD) {
+          if (m > 0) { q0 = grad[ip]; q1 = grad[ip + 1]; q2 = grad[ip + 2]; }
+        }
+        pair(n, X0, X1, X2, dX0, dX1, dX2, q0, q1, q2);
+        if constexpr (GRAD) { grad[ip] = q0; grad[ip + 1] = q1; grad[ip + 2] = q2; }
       }
     }
     if constexpr (GRAD) {
@@ -514,12 +549,23 @@ __device__ __forceinline__ bool ba_eval(const Layout& L, const S* x, const S* d,
       }
       slope_out = (r[11] * inv_s + gabsX * sums[1]) + dv + di;
     }
-    for (int n = tid; n < N; n += BLOCK) {
-      S* gp = grad + L.pt(n);
+    if constexpr (PPT > 0) {
 #pragma unroll
-      for (int c = 0; c < 3; ++c) {
-        const S X = trial_value<TRIAL>(x, d, alpha, L.pt(n) + c);
-        gp[c] = gp[c] * inv_s + sgn(X) * gabsX;
+      for (int u = 0; u < PPT; ++u) {
+        const int n = tid + u * BLOCK;
+        if (n < N) {
+#pragma unroll
+          for (int c = 0; c < 3; ++c) grad[L.pt(n) + c] = Gr[u][c] * inv_s + sgn(Xr[u][c]) * gabsX;
+        }
+      }
+    } else {
+      for (int n = tid; n < N; n += BLOCK) {
+        S* gp = grad + L.pt(n);
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+          const S X = trial_value<TRIAL>(x, d, alpha, L.pt(n) + c);
+          gp[c] = gp[c] * inv_s + sgn(X) * gabsX;
+        }
       }
     }
     for (int q = tid; q < 6 * (M - 1); q += BLOCK) {

@@ -558,7 +558,9 @@ __device__ __forceinline__ void compact_products_fused(int P, int Pv, int nh, co
   }
 }
 
-template <int MODE, bool GV, int RES, bool XL>  // XL: GV mode with x, d and the objective's gradient in LDS
+// XL: GV mode with x, d and the objective's gradient in LDS.  PPT > 0: the objective keeps
+// each thread's (<= PPT) points in registers across the view sweep (ba_eval).
+template <int MODE, bool GV, int RES, bool XL, int PPT>
 __global__ __launch_bounds__(kWave * solve_waves(GV), DAVA_SOLVE_WAVES_PER_EU) void bfgs_ba_solve_kernel(SolveArgs a) {
   static_assert(!XL || GV, "XL is a global-vector-mode variant");
   constexpr int NW = solve_waves(GV);
@@ -647,7 +649,7 @@ __global__ __launch_bounds__(kWave * solve_waves(GV), DAVA_SOLVE_WAVES_PER_EU) v
     if (have_next) {
       E = E_next;
     } else {
-      ba_eval<true, false, false, false, false, RES, float, NW>(L, x, nullptr, 0.f, obs, vis, grad_buf(g), views, vpart,
+      ba_eval<true, false, false, false, false, RES, float, NW, PPT>(L, x, nullptr, 0.f, obs, vis, grad_buf(g), views, vpart,
                                                                 scratch, buf, E, unused);
       publish(g);
       ++evals;
@@ -790,7 +792,7 @@ __global__ __launch_bounds__(kWave * solve_waves(GV), DAVA_SOLVE_WAVES_PER_EU) v
       // next iterate's gradient) and phi'(alpha) = d . grad (DOT).
       const bool known_same = DAVA_TRIAL_CHECK && al <= nomove_al;  // uniform
       if (!known_same &&
-          ba_eval<true, !DAVA_TRIAL_DOT, true, DAVA_TRIAL_DOT, DAVA_TRIAL_CHECK, RES, float, NW>(
+          ba_eval<true, !DAVA_TRIAL_DOT, true, DAVA_TRIAL_DOT, DAVA_TRIAL_CHECK, RES, float, NW, PPT>(
               L, x, d, al, obs, vis, grad_buf(gp), views, vpart, scratch, buf, fa, dfa)) {
         ++evals;
         last_same = false;
@@ -867,7 +869,7 @@ __global__ __launch_bounds__(kWave * solve_waves(GV), DAVA_SOLVE_WAVES_PER_EU) v
   for (int i = tid; i < P; i += BLOCK) xo[i] = x[i];
   if (a.err_out) {
     float e2 = 0.f;
-    ba_eval<false, false, false, false, false, RES, float, NW>(L, x, nullptr, 0.f, obs, vis, nullptr, views, vpart, scratch, buf,
+    ba_eval<false, false, false, false, false, RES, float, NW, PPT>(L, x, nullptr, 0.f, obs, vis, nullptr, views, vpart, scratch, buf,
                                                    e2, unused);
     if (tid == 0) a.err_out[b] = e2;
   }
@@ -1040,12 +1042,28 @@ extern "C" int dava_ba_solve_plan(const DavaScene* scene, const DavaSolverConfig
   return plan->lds_bytes > kMaxLds || kcap > kMaxCompactEntries ? DAVA_ERR_UNSUPPORTED : DAVA_OK;
 }
 
+template <int MODE, bool GV, int RES, bool XL, int PPT>
+static void launch_solve_ppt(const SolveArgs& a, int B, int lds, hipStream_t s) {
+  if (lds > 64 * 1024)
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(bfgs_ba_solve_kernel<MODE, GV, RES, XL, PPT>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+  hipLaunchKernelGGL((bfgs_ba_solve_kernel<MODE, GV, RES, XL, PPT>), dim3(B), dim3(kWave * solve_waves(GV)), lds, s, a);
+}
+
+// Points per thread held in registers by the objective: one for the LDS-mode kernels (C1-C3:
+// N <= 256; C3 +12% over re-reading x, d and the gradient from LDS per view).  Larger N, GV
+// mode and DAVA_NO_PPT take the re-reading variant: eight points per thread at C5 spill
+// (1 KB of scratch per lane) and ran 42% slower.
+template <bool GV, bool XL>
+constexpr int kRegisterPoints = GV ? 0 : 1;
+
 template <int MODE, bool GV, int RES, bool XL>
 static void launch_solve_res(const SolveArgs& a, int B, int lds, hipStream_t s) {
-  if (lds > 64 * 1024)
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(bfgs_ba_solve_kernel<MODE, GV, RES, XL>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-  hipLaunchKernelGGL((bfgs_ba_solve_kernel<MODE, GV, RES, XL>), dim3(B), dim3(kWave * solve_waves(GV)), lds, s, a);
+  constexpr int R = kRegisterPoints<GV, XL>;
+  if (R > 0 && a.L.N <= R * kWave * solve_waves(GV) && getenv("DAVA_NO_PPT") == nullptr)
+    launch_solve_ppt<MODE, GV, RES, XL, R>(a, B, lds, s);
+  else
+    launch_solve_ppt<MODE, GV, RES, XL, 0>(a, B, lds, s);
 }
 
 template <int MODE, bool GV, bool XL = false>
