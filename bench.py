@@ -50,7 +50,7 @@ def parse():
     p.add_argument("--residual", choices=["reprojection", "ray_angle"], default="reprojection",
                    help="ray_angle: CalibrationNetwork's error (pinhole only; not the headline metric)")
     p.add_argument("--seed", type=int, default=20251015 + 3000)
-    p.add_argument("--cpu-sample", type=int, default=12, help="problems timed on the CPU oracle (0 = skip)")
+    p.add_argument("--cpu-sample", type=int, default=32, help="problems timed on the CPU oracle (0 = skip)")
     p.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "pmc_traffic.json"))
     return p.parse_args()
 

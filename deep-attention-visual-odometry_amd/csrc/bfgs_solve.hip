@@ -998,7 +998,7 @@ static size_t compact_history_bytes(const DavaScene* s, const DavaSolverConfig* 
 // on-chip.  Default: whatever fits beside the problem image without dropping below two
 // workgroups per CU (80 KiB each); DAVA_LDS_HISTORY=n overrides (A/B and tests; 0 = all in
 // HBM; values past one workgroup's LDS are clamped).
-constexpr int kLdsPerWorkgroupAt2 = 80 * 1024;
+constexpr int kLdsPerWorkgroupAt2 = kMaxLds / DAVA_SOLVE_WAVES_PER_EU;  // 80 KiB at 2 workgroups per CU
 static int lds_history_entries(const DavaScene* s, int kcap, bool gv) {
 #ifdef DAVA_COMPACT_TWO_PASS
   return 0;
