@@ -31,6 +31,28 @@
 
 namespace dava {
 
+// Diagnostic builds only (DAVA_PHASE_TIMING): thread 0 of every workgroup adds the shader
+// cycles of each section of ba_eval (float instantiations) to g_eval_cycles.
+#ifndef DAVA_PHASE_TIMING
+#define DAVA_PHASE_TIMING 0
+#endif
+constexpr int kEvalSections = 6;  // view constants, point sums, setup, pair sweep, final sums, gradient assembly
+#if DAVA_PHASE_TIMING
+__device__ unsigned long long g_eval_cycles[kEvalSections];
+#define DAVA_ESTAMP(i)                                                           \
+  do {                                                                           \
+    if (std::is_same<S, float>::value && threadIdx.x == 0) {                     \
+      const unsigned long long t1_ = clock64();                                  \
+      atomicAdd(&g_eval_cycles[i], t1_ - et0_);                                  \
+      et0_ = t1_;                                                                \
+    }                                                                            \
+  } while (0)
+#else
+#define DAVA_ESTAMP(i) \
+  do {                 \
+  } while (0)
+#endif
+
 struct Layout {
   int M, N, P, distort;
   __device__ __forceinline__ int pt(int n) const { return 3 + 3 * n; }
@@ -186,12 +208,17 @@ __device__ __forceinline__ bool ba_eval(const Layout& L, const S* x, const S* d,
   static_assert(!CHECK || TRIAL, "CHECK needs a trial point");
   constexpr int PR = PPT > 0 ? PPT : 1;
   S Xr[PR][3], Dr[PR][3], Gr[PR][3];  // PPT > 0: this thread's points (n = tid + u BLOCK)
+#if DAVA_PHASE_TIMING
+  unsigned long long et0_ = clock64();
+#endif
   const int tid = threadIdx.x;
   const int lane = tid & (kWave - 1);
   const int wave = tid / kWave;
   const int M = L.M, N = L.N;
 
-  // 1. per-view rotation constants (views 1..M-1), one thread per view
+  // 1. per-view rotation constants (views 1..M-1), one thread per view; the same thread adds
+  //    its view's |t| (and sgn(t) dt) to the scale-normalisation sums of step 2
+  S t_abs = 0.f, t_dir = 0.f;
   for (int m = 1 + tid; m < M; m += BLOCK) {
     S* v = views + (m - 1) * kViewStride;
     const int r = L.rot(m), t = L.tr(m);
@@ -206,19 +233,28 @@ __device__ __forceinline__ bool ba_eval(const Layout& L, const S* x, const S* d,
     v[VRCP] = rcp;
     v[VAP] = rcp * (B - 2.0f * A);       // d/dth (1-cos)/th^2, reference backward form
     v[VTC] = th * sinc_slope(th);        // d/dth sin(th)/th
-    v[VT0] = trial_value<TRIAL>(x, d, alpha, t + 0);
-    v[VT1] = trial_value<TRIAL>(x, d, alpha, t + 1);
-    v[VT2] = trial_value<TRIAL>(x, d, alpha, t + 2);
+    const S t0 = trial_value<TRIAL>(x, d, alpha, t + 0);
+    const S t1 = trial_value<TRIAL>(x, d, alpha, t + 1);
+    const S t2 = trial_value<TRIAL>(x, d, alpha, t + 2);
+    v[VT0] = t0; v[VT1] = t1; v[VT2] = t2;
+    t_abs += fabs_(t0);
+    t_abs += fabs_(t1);
+    t_abs += fabs_(t2);
     if constexpr (SLOPE) {
       const S d0 = d[r], d1 = d[r + 1], d2 = d[r + 2];
       v[VDW0] = d0; v[VDW1] = d1; v[VDW2] = d2;
       v[VDTH] = (w0 * d0 + w1 * d1 + w2 * d2) * rcp;
       v[VDT0] = d[t]; v[VDT1] = d[t + 1]; v[VDT2] = d[t + 2];
+      t_dir += sgn(t0) * d[t];
+      t_dir += sgn(t1) * d[t + 1];
+      t_dir += sgn(t2) * d[t + 2];
     }
   }
 
+  DAVA_ESTAMP(0);
   // 2. scale normalisation s = (mean|X| N + mean|t| M)/(N+M), and its slope
-  S sums[3] = {0.f, 0.f, 0.f};  // sum|X|, sum sgn(X) dX (SLOPE or DOT), moved (CHECK)
+  // sum|X|, sum sgn(X) dX (SLOPE or DOT), moved (CHECK), sum|t|, sum sgn(t) dt (SLOPE)
+  S sums[5] = {0.f, 0.f, 0.f, t_abs, t_dir};
   bool moved = false;
   auto point_sums = [&](int n, S (&Xp)[3], S (&Dp)[3]) {
 #pragma unroll
@@ -246,22 +282,15 @@ __device__ __forceinline__ bool ba_eval(const Layout& L, const S* x, const S* d,
       moved |= trial_value<true>(x, d, alpha, i) != x[i];
     }
     sums[2] = moved ? 1.f : 0.f;
-    block_sum<3, NW>(sums, scratch, buf);
-  } else if constexpr (SLOPE || DOT) {
-    block_sum<2, NW>(reinterpret_cast<S(&)[2]>(sums), scratch, buf);
-  } else {
-    block_sum<1, NW>(reinterpret_cast<S(&)[1]>(sums), scratch, buf);
   }
+  block_sum<5, NW>(sums, scratch, buf);
   buf ^= 1;  // (this barrier also publishes the view constants)
+  DAVA_ESTAMP(1);
   if constexpr (CHECK) {
     if (sums[2] == 0.f) return false;  // uniform: every thread holds the same sums
   }
-  S tsum = 0.f, tdsum = 0.f;
-  for (int i = L.tr(1); i < L.tr(1) + 3 * (M - 1); ++i) {
-    const S t = trial_value<TRIAL>(x, d, alpha, i);
-    tsum += fabs_(t);
-    if constexpr (SLOPE) tdsum += sgn(t) * d[i];
-  }
+  const S tsum = sums[3], tdsum = sums[4];
+  (void)tdsum;
   const float fN = (float)N, fM = (float)M, fNM = (float)(N + M);
   const S ps = sums[0] / (3.0f * fN);
   const S cs = tsum / (3.0f * (float)(M - 1));
@@ -307,6 +336,7 @@ __device__ __forceinline__ bool ba_eval(const Layout& L, const S* x, const S* d,
   S gsx = 0.f;                          // sum gX~ . X  (scale path)
   S gdx = 0.f;                          // DOT: sum gX~ . dX
 
+  DAVA_ESTAMP(2);
   // 4. sweep views (outer) x own points (inner)
   for (int m = 0; m < M; ++m) {
     const S* v = views + (m > 0 ? (m - 1) * kViewStride : 0);
@@ -499,30 +529,25 @@ __device__ __forceinline__ bool ba_eval(const Layout& L, const S* x, const S* d,
           const S w = wave_sum(vg[k]);
           if (lane == 0) vpart[(m * NW + wave) * kViewPart + k] = w;
         }
+        // scale path, translation part: sum_m g_t~ . t (this thread's share) joins gsx in the
+        // final block reduction
+        gsx += vg[4] * v[VT0] + vg[5] * v[VT1] + vg[6] * v[VT2];
       }
     }
   }
 
+  DAVA_ESTAMP(3);
   // 5. block reduction of error, slope, intrinsics gradient and scale-path sum
   if constexpr (GRAD) {
     S r[12] = {e_loc, sl_loc, gin[0], gin[1], gin[2], gin[3], gin[4], gin[5], gin[6], gin[7], gsx, gdx};
     if constexpr (DOT) block_sum<12, NW>(r, scratch, buf);
     else block_sum<11, NW>(reinterpret_cast<S(&)[11]>(r), scratch, buf);
     buf ^= 1;
+    DAVA_ESTAMP(4);
     E_out = r[0];
     slope_out = r[1];
-    // scale path: s = (ps N + cs M)/(N+M); X~ = X/s, t~ = t/s
-    S gst = 0.f;  // sum g_t~ . t
-    for (int m = 1; m < M; ++m) {
-      const S* v = views + (m - 1) * kViewStride;
-#pragma unroll
-      for (int c = 0; c < 3; ++c) {
-        const S* q = vpart + (m * NW) * kViewPart + 4 + c;
-        const S g = wave_partials_total<NW>(q, kViewPart);
-        gst += g * v[VT0 + c];
-      }
-    }
-    const S gs = -(r[10] + gst) * inv_s * inv_s;
+    // scale path: s = (ps N + cs M)/(N+M); X~ = X/s, t~ = t/s.  r[10] = sum gX~ . X + sum g_t~ . t
+    const S gs = -r[10] * inv_s * inv_s;
     const S g_ps = gs * fN / fNM, g_cs = gs * fM / fNM;
     const S gabsX = g_ps / (3.0f * fN);
     const S gabsT = g_cs / (3.0f * (float)(M - 1));
@@ -590,6 +615,7 @@ __device__ __forceinline__ bool ba_eval(const Layout& L, const S* x, const S* d,
       }
     }
     __syncthreads();
+    DAVA_ESTAMP(5);
   } else {
     S r[2] = {e_loc, sl_loc};
     if constexpr (SLOPE) block_sum<2, NW>(r, scratch, buf);

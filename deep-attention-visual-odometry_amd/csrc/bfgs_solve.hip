@@ -1122,6 +1122,10 @@ extern "C" int dava_ba_solve(const DavaScene* scene, const DavaSolverConfig* con
   const size_t ph_bytes = (size_t)scene->batch * kPhases * sizeof(unsigned long long);
   if (hipMalloc(&a.phase_cycles, ph_bytes) != hipSuccess) return DAVA_ERR_LAUNCH;
   (void)hipMemsetAsync(a.phase_cycles, 0, ph_bytes, s);
+  {
+    const unsigned long long zero[kEvalSections] = {};
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_eval_cycles), zero, sizeof(zero));
+  }
 #endif
   if (mode == DAVA_HESSIAN_DENSE) {
     if (xl) launch_solve<DAVA_HESSIAN_DENSE, true, true>(a, scene->batch, lds, s, scene->residual);
@@ -1146,6 +1150,13 @@ extern "C" int dava_ba_solve(const DavaScene* scene, const DavaSolverConfig* con
       for (int i = 0; i < kPhases; ++i) avg[i] += (double)h[(size_t)b * kPhases + i] / scene->batch;
     fprintf(stderr, "[dava phase cycles / problem]");
     for (int i = 0; i < kPhases; ++i) fprintf(stderr, " %s=%.0f (%.1f%%)", names[i], avg[i], 100.0 * avg[i] / avg[kPhases - 1]);
+    fprintf(stderr, "\n");
+    unsigned long long ev[kEvalSections] = {};
+    (void)hipMemcpyFromSymbol(ev, HIP_SYMBOL(g_eval_cycles), sizeof(ev));
+    static const char* enames[kEvalSections] = {"view_constants", "point_sums", "setup", "pair_sweep", "final_sums",
+                                                "gradient_assembly"};
+    fprintf(stderr, "[dava objective cycles / problem]");
+    for (int i = 0; i < kEvalSections; ++i) fprintf(stderr, " %s=%.0f", enames[i], (double)ev[i] / scene->batch);
     fprintf(stderr, "\n");
     free(h);
   }

@@ -1,0 +1,13 @@
+#!/bin/bash
+# Objective restructuring (|t| sums and the scale-path translation term folded into the block
+# reductions): GPU tests, interleaved A/B against the previous build, section stamps
+cd ${GRAFT_REPO_ROOT:-$(pwd)}
+V=$PWD/deep-attention-visual-odometry_amd/build
+timeout -k 10 600 python3 -u -m pytest tests/test_gpu_solver.py tests/test_gpu_objective.py tests/test_gpu_solve_grad.py \
+  -q --timeout 300 --timeout-method thread > gpurun_out/gpu_tests10.log 2>&1
+rc=$?; echo "tests exit $rc"; tail -3 gpurun_out/gpu_tests10.log
+[ $rc -le 1 ] || exit $rc
+tools/ab_env.sh "c3:" "c3prev:DAVA_LIB=$V/var_prev/libdava_ba.so" "c3:" "c3prev:DAVA_LIB=$V/var_prev/libdava_ba.so" || exit 1
+BENCH_ARGS="--steps 2 --warmup 1 --batch 256 --views 16 --points 4096 --no-distortion" \
+  tools/ab_env.sh "c5:" "c5prev:DAVA_LIB=$V/var_prev/libdava_ba.so" || exit 1
+DAVA_LIB=$V/var_phase/libdava_ba.so timeout -k 10 300 python3 bench.py --cpu-sample 0 --steps 1 --warmup 0 2>&1 | grep -E "cycles" | cut -c1-400
