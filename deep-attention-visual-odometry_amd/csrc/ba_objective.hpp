@@ -63,31 +63,32 @@ struct Layout {
 
 // ---- Taylor-branched ratios, same thresholds and series as the reference ----
 // (templated on the scalar: float, or Dual for second derivatives, dava_dual.hpp)
+// sx, cx: sin x and cos x, computed once by the caller (sincos_)
 template <typename S>
-__device__ __forceinline__ S sinc(S x) {
+__device__ __forceinline__ S sinc(S x, S sx) {
   if (fabs_(x) < 0.01f) {
     const S x2 = x * x, x4 = x2 * x2, x6 = x4 * x2;
     return 1.0f - x2 / 6.0f + x4 / 120.0f - x6 / 5040.0f;
   }
-  return sin_(x) / x;
+  return sx / x;
 }
 template <typename S>
-__device__ __forceinline__ S sinc_slope(S x) {  // cos/x^2 - sin/x^3
+__device__ __forceinline__ S sinc_slope(S x, S sx, S cx) {  // cos/x^2 - sin/x^3
   const S x2 = x * x;
   if (fabs_(x) < 0.01f) {
     const S x4 = x2 * x2, x6 = x4 * x2;
     return -1.0f / 3.0f + x2 / 30.0f - x4 / 840.0f + x6 / 45360.0f;
   }
-  return cos_(x) / x2 - sin_(x) / (x * x2);
+  return cx / x2 - sx / (x * x2);
 }
 template <typename S>
-__device__ __forceinline__ S versine_ratio(S x) {  // (1 - cos x)/x^2
+__device__ __forceinline__ S versine_ratio(S x, S cx) {  // (1 - cos x)/x^2
   const S x2 = x * x;
   if (fabs_(x) < 0.05f) {
     const S x4 = x2 * x2, x6 = x4 * x2;
     return 0.5f - x2 / 24.0f + x4 / 720.0f - x6 / 40320.0f;
   }
-  return (1.0f - cos_(x)) / x2;
+  return (1.0f - cx) / x2;
 }
 
 // ---- per-view constants, kept in LDS (one row of kViewStride floats per view >= 1) ----
@@ -226,13 +227,15 @@ __device__ __forceinline__ bool ba_eval(const Layout& L, const S* x, const S* d,
     const S w1 = trial_value<TRIAL>(x, d, alpha, r + 1);
     const S w2 = trial_value<TRIAL>(x, d, alpha, r + 2);
     const S th = sqrt_(w0 * w0 + w1 * w1 + w2 * w2);
-    const S A = versine_ratio(th), B = sinc(th);
+    S sth, cth;
+    sincos_(th, sth, cth);
+    const S A = versine_ratio(th, cth), B = sinc(th, sth);
     const S rcp = th == 0.0f ? S(0.0f) : 1.0f / th;
     v[VW0] = w0; v[VW1] = w1; v[VW2] = w2;
-    v[VCOS] = cos_(th); v[VA] = A; v[VB] = B; v[VSIN] = sin_(th);
+    v[VCOS] = cth; v[VA] = A; v[VB] = B; v[VSIN] = sth;
     v[VRCP] = rcp;
     v[VAP] = rcp * (B - 2.0f * A);       // d/dth (1-cos)/th^2, reference backward form
-    v[VTC] = th * sinc_slope(th);        // d/dth sin(th)/th
+    v[VTC] = th * sinc_slope(th, sth, cth);  // d/dth sin(th)/th
     const S t0 = trial_value<TRIAL>(x, d, alpha, t + 0);
     const S t1 = trial_value<TRIAL>(x, d, alpha, t + 1);
     const S t2 = trial_value<TRIAL>(x, d, alpha, t + 2);

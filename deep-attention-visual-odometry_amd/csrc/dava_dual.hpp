@@ -79,6 +79,14 @@ __device__ __forceinline__ Dual atan2_(Dual y, Dual x) {
   const float den = x.v * x.v + y.v * y.v;
   return {atan2f(y.v, x.v), (x.v * y.t - y.v * x.t) / den};
 }
+// sin and cos of one argument through one range reduction
+__device__ __forceinline__ void sincos_(float x, float& s, float& c) { sincosf(x, &s, &c); }
+__device__ __forceinline__ void sincos_(Dual x, Dual& s, Dual& c) {
+  float sv, cv;
+  sincosf(x.v, &sv, &cv);
+  s = {sv, cv * x.t};
+  c = {cv, -sv * x.t};
+}
 __device__ __forceinline__ Dual fmul_rn(Dual a, Dual b) { return a * b; }
 __device__ __forceinline__ Dual fadd_rn(Dual a, Dual b) { return a + b; }
 __device__ __forceinline__ float value_of(Dual x) { return x.v; }
