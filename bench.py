@@ -50,6 +50,10 @@ def parse():
     p.add_argument("--residual", choices=["reprojection", "ray_angle"], default="reprojection",
                    help="ray_angle: CalibrationNetwork's error (pinhole only; not the headline metric)")
     p.add_argument("--seed", type=int, default=20251015 + 3000)
+    p.add_argument("--error-threshold", type=float, default=-1.0,
+                   help=">= 0: stop problems by the reference's rules (e.g. 1e-4 with --minimum-step 1e-8 "
+                        "--iterations 1000); not the headline metric, roofline then null")
+    p.add_argument("--minimum-step", type=float, default=-1.0)
     p.add_argument("--cpu-sample", type=int, default=32, help="problems timed on the CPU oracle (0 = skip)")
     p.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "pmc_traffic.json"))
     return p.parse_args()
@@ -91,7 +95,8 @@ def cpu_baseline(args, x0, obs, vis, p):
         fn = objective.ReprojectionClosure(obs[:n], vis[:n], args.views, args.points, not args.no_distortion)
     threads = torch.get_num_threads()
     t = time.perf_counter()
-    solver.bfgs_solve(x0[:n], fn, iterations=args.iterations, error_threshold=-1.0, minimum_step=-1.0)
+    solver.bfgs_solve(x0[:n], fn, iterations=args.iterations, error_threshold=args.error_threshold,
+                      minimum_step=args.minimum_step)
     dt = time.perf_counter() - t
     return {
         "value": n / dt,
@@ -154,7 +159,8 @@ def main():
             e1 = torch.cuda.Event(enable_timing=True)
             e0.record(stream)
         x, _, status = native_ops.ba_solve(x0, obs, vis, args.views, args.points, distortion,
-                                           iterations=args.iterations, error_threshold=-1.0, minimum_step=-1.0,
+                                           iterations=args.iterations, error_threshold=args.error_threshold,
+                                           minimum_step=args.minimum_step,
                                            hessian_mode=mode, want_status=True, workspace=workspace,
                                            residual=residual)
         if timed:
@@ -191,7 +197,8 @@ def main():
     finite = bool(torch.isfinite(x).all().item())
 
     if rank == 0:
-        headline = (b, args.views, args.points, distortion, ray, args.iterations) == (8192, 4, 256, True, False, 100)
+        fixed_k = args.error_threshold < 0 and args.minimum_step < 0  # every problem runs exactly K iterations
+        headline = fixed_k and (b, args.views, args.points, distortion, ray, args.iterations) == (8192, 4, 256, True, False, 100)
         value = world * b * args.steps / elapsed
         plan = native_ops.solve_plan(b, args.views, args.points, distortion, mode, args.iterations, residual)
         if args.mode == "dense":
@@ -199,7 +206,7 @@ def main():
         else:
             algo = b * compact_algorithmic_bytes(p, mn, args.iterations, plan["lds_history_entries"])
         roofline = None
-        if algo is not None:
+        if algo is not None and fixed_k:
             achieved = algo / (launch_ms * 1e-3) / 1e9
             traffic = None
             try:
@@ -222,7 +229,7 @@ def main():
         line = {
             "metric": f"BA problems/sec (B={b} per GPU, {args.views} views x {args.points} pts"
                       f"{', Brown-Conrady' if distortion else ''}{', ray-angle residual' if ray else ''}, "
-                      f"K={args.iterations} BFGS iterations)",
+                      f"K={args.iterations} BFGS iterations{'' if fixed_k else ' max, reference stopping rules'})",
             "value": round(value, 2),
             "unit": "problems/s",
             "n_gpus": world,
@@ -239,7 +246,8 @@ def main():
                             f": batch={b} per GPU, {args.views} views x {args.points} pts, "
                             f"{'pinhole+Brown-Conrady' if distortion else 'pinhole'}"
                             f"{' ray-angle residual' if ray else ''}, P={p}, "
-                            f"K={args.iterations} fixed iterations, strong Wolfe (c1=1e-4, c2=0.9)",
+                            f"K={args.iterations} {'fixed iterations' if fixed_k else f'iterations max, error <= {args.error_threshold}, step <= {args.minimum_step}'}"
+                            f", strong Wolfe (c1=1e-4, c2=0.9)",
                 "global_batch": world * b,
                 "num_parameters": p,
                 "iterations": args.iterations,
@@ -250,6 +258,7 @@ def main():
             "cpu_baseline": cpu,
             "diagnostics": {"objective_evals_per_iteration": round(evals, 3),
                             "line_search_trials_per_iteration": round(trials, 3),
+                            "mean_steps_per_problem": round(st[:, 0].double().mean().item(), 2),
                             "all_finite": finite, "plan": plan},
         }
         print(json.dumps(line), flush=True)

@@ -45,6 +45,7 @@ struct SolveArgs {
   int lcap;       // COMPACT, LDS mode: entries 0 .. lcap-1 live in LDS instead of HBM
   float* vecs;    // GV mode: B x kVectors x Pv floats (else unused)
   unsigned long long* phase_cycles;  // DAVA_PHASE_TIMING builds: B x kPhases (else null)
+  int* queue;     // work-queue counter (zeroed before the launch), or null: problem = blockIdx.x
 };
 
 struct LdsCarve {
@@ -569,313 +570,326 @@ __global__ __launch_bounds__(kWave * solve_waves(GV), DAVA_SOLVE_WAVES_PER_EU) v
   const Layout L = a.L;
   const int P = L.P, M = L.M, N = L.N;
   const int Pv = a.Pv;
-  const int b = blockIdx.x;
   const int tid = threadIdx.x;
-  const int lcap = MODE == DAVA_HESSIAN_COMPACT && !GV ? a.lcap : 0;
-  const LdsCarve cv = carve_lds(M, N, Pv, MODE == DAVA_HESSIAN_COMPACT ? a.kcap : 0, GV, lcap, XL);
-  float* LH = lds + cv.hist;  // LDS-resident history entries 0 .. lcap-1
-  float* vb0 = GV ? a.vecs + (size_t)b * kVectors * Pv : lds;
-  float* x = (GV && !XL ? vb0 : lds) + cv.x;
-  float* d = (GV && !XL ? vb0 : lds) + cv.d;
-  float* ge = lds + cv.ge;  // XL: the objective's gradient output, copied to g / gp after each evaluation
-  // the objective's gradient target and its publication to the workspace vector `dst`
-  auto grad_buf = [&](float* dst) { return XL ? ge : dst; };
-  auto publish = [&](float* dst) {
-    if constexpr (XL) {
-      for (int i = tid; i < P; i += BLOCK) dst[i] = ge[i];
+  // Work queue (a.queue != null): the grid holds as many workgroups as are resident at once and
+  // each takes the next problem when it finishes one, so a problem that stops early or runs a
+  // long line search never leaves its slot idle.  Without a queue: problem = blockIdx.x.
+  __shared__ int queued_problem;
+  for (int b = blockIdx.x;;) {
+    if (a.queue) {
+      __syncthreads();  // every thread is done with the previous problem's LDS image
+      if (tid == 0) queued_problem = atomicAdd(a.queue, 1);
       __syncthreads();
+      b = queued_problem;
+      if (b >= a.B) break;
     }
-  };
-  float* g = vb0 + cv.g0;
-  float* gp = vb0 + cv.g1;
-  float* hcoef = lds + cv.hcoef;
-  float* hrho = lds + cv.hrho;
-  float* hc = lds + cv.hc;
-  float* s_cur = vb0 + cv.s0;
-  float* s_pend = vb0 + cv.s1;
-  float* hy_new = vb0 + cv.hy0;
-  float* hy_pend = vb0 + cv.hy1;
-  float* hg = vb0 + cv.hg;
-  float* views = lds + cv.views;
-  float* vpart = lds + cv.vpart;
-  float* scratch = lds + cv.scratch;
-  const int MN = M * N;
-  const float* obs = GV ? a.obs + (size_t)b * 2 * MN : lds + cv.obs;
-  const uint8_t* vis = GV ? a.vis + (size_t)b * MN : reinterpret_cast<uint8_t*>(lds) + cv.vis_bytes_off;
-
-  // ---- stage the problem into LDS (zero the vector pads) ----
-  const float* x0 = a.x0 + (size_t)b * P;
-  for (int i = tid; i < Pv; i += BLOCK) {
-    x[i] = i < P ? x0[i] : 0.f;
-    d[i] = g[i] = gp[i] = s_cur[i] = s_pend[i] = hy_new[i] = hy_pend[i] = hg[i] = 0.f;
-  }
-  if (!GV) {
-    float* o = lds + cv.obs;
-    uint8_t* v = reinterpret_cast<uint8_t*>(lds) + cv.vis_bytes_off;
-    const float* ob = a.obs + (size_t)b * 2 * MN;
-    for (int i = tid; i < 2 * MN; i += BLOCK) o[i] = ob[i];
-    const uint8_t* vbb = a.vis + (size_t)b * MN;
-    for (int i = tid; i < MN; i += BLOCK) v[i] = vbb[i] ? 1 : 0;
-  }
-  __syncthreads();
-
-  float* H = nullptr;   // DENSE: this problem's P x Pld inverse Hessian
-  float* SH = nullptr;  // COMPACT: history rows S[kcap][Pv], W[kcap][Pv]
-  float* WH = nullptr;
-  if (MODE == DAVA_HESSIAN_DENSE) {
-    H = a.hess ? a.hess + (size_t)b * P * a.Pld : nullptr;
-  } else if (a.hess) {
-    SH = a.hess + (size_t)b * 2 * a.kcap * Pv;
-    WH = SH + (size_t)a.kcap * Pv;
-  }
-  int buf = 0;
-  bool materialized = false;
-  float gamma0 = 1.f, pend_rho = 0.f, pend_c = 1.f;
-  int steps = 0, reason = DAVA_STOP_ITERATIONS, evals = 0, trials = 0;
-  float E = 0.f, unused = 0.f;
-
-  // When the line search accepts the step it evaluated last, that trial (which also
-  // formed the full gradient) IS the evaluation at x_{k+1} = x_k + alpha d: same point,
-  // bit for bit, so the next iteration's objective + gradient are taken from it.
-  bool have_next = false;
-  float E_next = 0.f;
-#if DAVA_PHASE_TIMING
-  unsigned long long ph_acc[kPhases] = {0, 0, 0, 0, 0, 0, 0};
-  const unsigned long long ph_start = clock64();
-  unsigned long long ph_t0 = ph_start;
-#endif
-  for (int k = 0; k < a.iters; ++k) {
-    { float* t = g; g = gp; gp = t; }  // gp <- previous gradient; g <- (trial) gradient buffer
-    if (have_next) {
-      E = E_next;
-    } else {
-      ba_eval<true, false, false, false, false, RES, float, NW, PPT>(L, x, nullptr, 0.f, obs, vis, grad_buf(g), views, vpart,
-                                                                scratch, buf, E, unused);
-      publish(g);
-      ++evals;
-    }
-    DAVA_PHASE(0);
-    if (!(E > a.thr)) { reason = DAVA_STOP_ERROR; break; }
-
-    if (k == 0) {
-      // first step: no inverse Hessian yet, d = -g (bfgs_solver.py:152-155)
-      for (int i = tid; i < P; i += BLOCK) d[i] = -1.0f * g[i];
-      __syncthreads();
-    } else {
-      float r[4] = {0, 0, 0, 0};
-      float rho, c, sg, hyg;
-      if (k == 1) {
-        // H_0 = gamma I, gamma from N&W eq. 6.20 (bfgs_solver.py:159-167, 217-233)
-        for (int i = tid; i < P; i += BLOCK) {
-          const float gi = g[i], yi = gi - gp[i], si = s_cur[i];
-          r[0] += si * yi; r[1] += yi * yi; r[2] += si * gi; r[3] += yi * gi;
-        }
-        block_sum<4, NW>(r, scratch, buf); buf ^= 1;
-        const float gamma = clamp_min(r[0] / clamp_min(r[1], 1e-5f), 1e-4f);
-        gamma0 = gamma;
-        rho = r[0] <= 0.f ? 0.f : 1.0f / r[0];
-        c = 1.0f + rho * (gamma * r[1]);
-        sg = r[2];
-        hyg = gamma * r[3];
-        for (int i = tid; i < P; i += BLOCK) {
-          const float gi = g[i], yi = gi - gp[i];
-          hy_new[i] = gamma * yi;
-          hg[i] = gamma * gi;
-        }
-        // (no barrier needed: each thread reads back only its own hy_new / hg below)
-      } else {
-#if DAVA_DIAG_NO_SWEEP  // timing-only build: H stays gamma0 I (results are wrong)
-        for (int i = tid; i < P; i += BLOCK) { hy_new[i] = gamma0 * (g[i] - gp[i]); hg[i] = gamma0 * g[i]; }
-#else
-        if constexpr (MODE == DAVA_HESSIAN_DENSE) {
-          dense_sweep<NW>(L, a.Pld, H, materialized, gamma0, s_pend, hy_pend, pend_rho, pend_c, g, gp, hy_new, hg);
-          materialized = true;
-        } else {
-#ifndef DAVA_COMPACT_TWO_PASS
-          const int G4 = (P + 3) / 4;
-          const int GM = (G4 + kWave - 1) / kWave;
-          if constexpr (NW != kWaves) {  // GV: workgroup-wide single pass, else two passes
-            const int GT = (G4 + kWave * NW - 1) / (kWave * NW);
-            const int nh = k - 1;
-            if (!wide_history_pass(Pv, a.kcap, GV))
-              compact_products<GV ? 8 : 1, NW>(P, Pv, nh, SH, WH, hcoef, hrho, hc, gamma0, g, gp, hy_new, hg);
-            else if (GT <= 1) compact_products_wide<1, NW>(P, Pv, nh, SH, WH, hrho, hc, gamma0, g, gp, hy_new, hg, scratch, buf);
-            else if (GT == 2) compact_products_wide<2, NW>(P, Pv, nh, SH, WH, hrho, hc, gamma0, g, gp, hy_new, hg, scratch, buf);
-            else if (GT == 3) compact_products_wide<3, NW>(P, Pv, nh, SH, WH, hrho, hc, gamma0, g, gp, hy_new, hg, scratch, buf);
-            else if (GT == 4) compact_products_wide<4, NW>(P, Pv, nh, SH, WH, hrho, hc, gamma0, g, gp, hy_new, hg, scratch, buf);
-            else if (GT == 5) compact_products_wide<5, NW>(P, Pv, nh, SH, WH, hrho, hc, gamma0, g, gp, hy_new, hg, scratch, buf);
-            else if (GT == 6) compact_products_wide<6, NW>(P, Pv, nh, SH, WH, hrho, hc, gamma0, g, gp, hy_new, hg, scratch, buf);
-            else compact_products_wide<7, NW>(P, Pv, nh, SH, WH, hrho, hc, gamma0, g, gp, hy_new, hg, scratch, buf);
-          } else
-          if (GM <= 1) compact_products_fused<1>(P, Pv, k - 1, SH, WH, LH, lcap, hrho, hc, gamma0, g, gp, hy_new, hg, s_pend, hy_pend, d, hg);
-          else if (GM == 2) compact_products_fused<2>(P, Pv, k - 1, SH, WH, LH, lcap, hrho, hc, gamma0, g, gp, hy_new, hg, s_pend, hy_pend, d, hg);
-          else if (GM == 3) compact_products_fused<3>(P, Pv, k - 1, SH, WH, LH, lcap, hrho, hc, gamma0, g, gp, hy_new, hg, s_pend, hy_pend, d, hg);
-          else if (GM == 4) compact_products_fused<4>(P, Pv, k - 1, SH, WH, LH, lcap, hrho, hc, gamma0, g, gp, hy_new, hg, s_pend, hy_pend, d, hg);
-          else
-#endif
-          // GV mode (very long rows, few resident waves): 8 column groups in flight per lane;
-          // the LDS-mode kernel keeps the lean loop (its register budget is the fused pass's)
-          compact_products<GV ? 8 : 1, NW>(P, Pv, k - 1, SH, WH, hcoef, hrho, hc, gamma0, g, gp, hy_new, hg);
-        }
-#endif
+    const int lcap = MODE == DAVA_HESSIAN_COMPACT && !GV ? a.lcap : 0;
+    const LdsCarve cv = carve_lds(M, N, Pv, MODE == DAVA_HESSIAN_COMPACT ? a.kcap : 0, GV, lcap, XL);
+    float* LH = lds + cv.hist;  // LDS-resident history entries 0 .. lcap-1
+    float* vb0 = GV ? a.vecs + (size_t)b * kVectors * Pv : lds;
+    float* x = (GV && !XL ? vb0 : lds) + cv.x;
+    float* d = (GV && !XL ? vb0 : lds) + cv.d;
+    float* ge = lds + cv.ge;  // XL: the objective's gradient output, copied to g / gp after each evaluation
+    // the objective's gradient target and its publication to the workspace vector `dst`
+    auto grad_buf = [&](float* dst) { return XL ? ge : dst; };
+    auto publish = [&](float* dst) {
+      if constexpr (XL) {
+        for (int i = tid; i < P; i += BLOCK) dst[i] = ge[i];
         __syncthreads();
-        DAVA_PHASE(1);
-        for (int i = tid; i < P; i += BLOCK) {
-          const float gi = g[i], yi = gi - gp[i], si = s_cur[i], hi = hy_new[i];
-          r[0] += si * yi; r[1] += hi * yi; r[2] += si * gi; r[3] += hi * gi;
-        }
-        block_sum<4, NW>(r, scratch, buf); buf ^= 1;
-        rho = r[0] <= 0.f ? 0.f : 1.0f / r[0];  // inverse_curvature (func_inverse_curvature.py:24-28)
-        c = 1.0f + rho * r[1];
-        sg = r[2];
-        hyg = r[3];
       }
-      // d = -H_k g,  H_k = H' + c (rho s) s^T - (rho s) (H'y)^T - (H'y) (rho s)^T
-      const float rsg = rho * sg;
-      for (int i = tid; i < P; i += BLOCK) {
-        const float sri = s_cur[i] * rho;
-        d[i] = -1.0f * (hg[i] + sri * (c * sg) - sri * hyg - hy_new[i] * rsg);
-      }
-      if constexpr (MODE == DAVA_HESSIAN_DENSE) {
-        // the new update becomes the pending one; recycle the old buffers
-        { float* t = s_pend; s_pend = s_cur; s_cur = t; }
-        { float* t = hy_pend; hy_pend = hy_new; hy_new = t; }
-        pend_rho = rho;
-        pend_c = c;
-      } else if (k - 1 < a.kcap) {
-        // append U_k = (s, H y, rho, c) to the history (entry k-1), on-chip if it is one of the first lcap
-        if (k - 1 < lcap) {
-          float* sr = LH + (size_t)2 * (k - 1) * Pv;
-          for (int i = tid; i < Pv; i += BLOCK) { sr[i] = s_cur[i]; sr[Pv + i] = hy_new[i]; }
-        } else {
-          float* sr = SH + (size_t)(k - 1) * Pv;
-          float* wr = WH + (size_t)(k - 1) * Pv;
-          for (int i = tid; i < Pv; i += BLOCK) { sr[i] = s_cur[i]; wr[i] = hy_new[i]; }
-        }
-        if (tid == 0) { hrho[k - 1] = rho; hc[k - 1] = c; }
-      }
-      __syncthreads();
-    }
+    };
+    float* g = vb0 + cv.g0;
+    float* gp = vb0 + cv.g1;
+    float* hcoef = lds + cv.hcoef;
+    float* hrho = lds + cv.hrho;
+    float* hc = lds + cv.hc;
+    float* s_cur = vb0 + cv.s0;
+    float* s_pend = vb0 + cv.s1;
+    float* hy_new = vb0 + cv.hy0;
+    float* hy_pend = vb0 + cv.hy1;
+    float* hg = vb0 + cv.hg;
+    float* views = lds + cv.views;
+    float* vpart = lds + cv.vpart;
+    float* scratch = lds + cv.scratch;
+    const int MN = M * N;
+    const float* obs = GV ? a.obs + (size_t)b * 2 * MN : lds + cv.obs;
+    const uint8_t* vis = GV ? a.vis + (size_t)b * MN : reinterpret_cast<uint8_t*>(lds) + cv.vis_bytes_off;
 
-    // ---- strong-Wolfe line search (wolfe_conditions.py:23-239) ----
-    float dphi0;
-    {
-      float r[1] = {0.f};
-      for (int i = tid; i < P; i += BLOCK) r[0] += d[i] * g[i];
-      block_sum<1, NW>(r, scratch, buf); buf ^= 1;
-      dphi0 = r[0];
+    // ---- stage the problem into LDS (zero the vector pads) ----
+    const float* x0 = a.x0 + (size_t)b * P;
+    for (int i = tid; i < Pv; i += BLOCK) {
+      x[i] = i < P ? x0[i] : 0.f;
+      d[i] = g[i] = gp[i] = s_cur[i] = s_pend[i] = hy_new[i] = hy_pend[i] = hg[i] = 0.f;
     }
-    DAVA_PHASE(2);
-    float a_lo = 0.f, a_hi = 0.f, al = 1.f, f_lo = E, f_hi = E, fa = E, dfa = dphi0;
-    float last_al = 0.f, last_fa = 0.f;
-    // Largest alpha seen whose trial point rounded back to x.  Rounding is monotone
-    // (0 <= a' <= a => |fl(a' d_i)| <= |fl(a d_i)| and fl(x_i + .) stays x_i), so every smaller
-    // trial is a no-move point too and needs neither evaluation nor the check: at fp32
-    // stagnation a bisection towards 0 runs ~150 such trials per line search (C2's slowest
-    // problems: thousands per solve).
-    float nomove_al = -1.0f;
-    bool widen = true, zoom = false, evaluated = false, last_same = false;
-    // trial gradients go into gp's buffer (g_prev is dead once d is formed)
-    const float lim = (-a.c2) * dphi0;
-    for (int t = 0; t < a.max_trials; ++t) {
-      if (!(widen || zoom)) break;
-      if (t > 0) {
-        if (widen) { a_hi = al; f_hi = fa; al = 2.0f * al; }
-        if (zoom) al = 0.5f * (a_lo + a_hi);
+    if (!GV) {
+      float* o = lds + cv.obs;
+      uint8_t* v = reinterpret_cast<uint8_t*>(lds) + cv.vis_bytes_off;
+      const float* ob = a.obs + (size_t)b * 2 * MN;
+      for (int i = tid; i < 2 * MN; i += BLOCK) o[i] = ob[i];
+      const uint8_t* vbb = a.vis + (size_t)b * MN;
+      for (int i = tid; i < MN; i += BLOCK) v[i] = vbb[i] ? 1 : 0;
+    }
+    __syncthreads();
+
+    float* H = nullptr;   // DENSE: this problem's P x Pld inverse Hessian
+    float* SH = nullptr;  // COMPACT: history rows S[kcap][Pv], W[kcap][Pv]
+    float* WH = nullptr;
+    if (MODE == DAVA_HESSIAN_DENSE) {
+      H = a.hess ? a.hess + (size_t)b * P * a.Pld : nullptr;
+    } else if (a.hess) {
+      SH = a.hess + (size_t)b * 2 * a.kcap * Pv;
+      WH = SH + (size_t)a.kcap * Pv;
+    }
+    int buf = 0;
+    bool materialized = false;
+    float gamma0 = 1.f, pend_rho = 0.f, pend_c = 1.f;
+    int steps = 0, reason = DAVA_STOP_ITERATIONS, evals = 0, trials = 0;
+    float E = 0.f, unused = 0.f;
+
+    // When the line search accepts the step it evaluated last, that trial (which also
+    // formed the full gradient) IS the evaluation at x_{k+1} = x_k + alpha d: same point,
+    // bit for bit, so the next iteration's objective + gradient are taken from it.
+    bool have_next = false;
+    float E_next = 0.f;
+  #if DAVA_PHASE_TIMING
+    unsigned long long ph_acc[kPhases] = {0, 0, 0, 0, 0, 0, 0};
+    const unsigned long long ph_start = clock64();
+    unsigned long long ph_t0 = ph_start;
+  #endif
+    for (int k = 0; k < a.iters; ++k) {
+      { float* t = g; g = gp; gp = t; }  // gp <- previous gradient; g <- (trial) gradient buffer
+      if (have_next) {
+        E = E_next;
+      } else {
+        ba_eval<true, false, false, false, false, RES, float, NW, PPT>(L, x, nullptr, 0.f, obs, vis, grad_buf(g), views, vpart,
+                                                                  scratch, buf, E, unused);
+        publish(g);
+        ++evals;
+      }
+      DAVA_PHASE(0);
+      if (!(E > a.thr)) { reason = DAVA_STOP_ERROR; break; }
+
+      if (k == 0) {
+        // first step: no inverse Hessian yet, d = -g (bfgs_solver.py:152-155)
+        for (int i = tid; i < P; i += BLOCK) d[i] = -1.0f * g[i];
+        __syncthreads();
+      } else {
+        float r[4] = {0, 0, 0, 0};
+        float rho, c, sg, hyg;
+        if (k == 1) {
+          // H_0 = gamma I, gamma from N&W eq. 6.20 (bfgs_solver.py:159-167, 217-233)
+          for (int i = tid; i < P; i += BLOCK) {
+            const float gi = g[i], yi = gi - gp[i], si = s_cur[i];
+            r[0] += si * yi; r[1] += yi * yi; r[2] += si * gi; r[3] += yi * gi;
+          }
+          block_sum<4, NW>(r, scratch, buf); buf ^= 1;
+          const float gamma = clamp_min(r[0] / clamp_min(r[1], 1e-5f), 1e-4f);
+          gamma0 = gamma;
+          rho = r[0] <= 0.f ? 0.f : 1.0f / r[0];
+          c = 1.0f + rho * (gamma * r[1]);
+          sg = r[2];
+          hyg = gamma * r[3];
+          for (int i = tid; i < P; i += BLOCK) {
+            const float gi = g[i], yi = gi - gp[i];
+            hy_new[i] = gamma * yi;
+            hg[i] = gamma * gi;
+          }
+          // (no barrier needed: each thread reads back only its own hy_new / hg below)
+        } else {
+  #if DAVA_DIAG_NO_SWEEP  // timing-only build: H stays gamma0 I (results are wrong)
+          for (int i = tid; i < P; i += BLOCK) { hy_new[i] = gamma0 * (g[i] - gp[i]); hg[i] = gamma0 * g[i]; }
+  #else
+          if constexpr (MODE == DAVA_HESSIAN_DENSE) {
+            dense_sweep<NW>(L, a.Pld, H, materialized, gamma0, s_pend, hy_pend, pend_rho, pend_c, g, gp, hy_new, hg);
+            materialized = true;
+          } else {
+  #ifndef DAVA_COMPACT_TWO_PASS
+            const int G4 = (P + 3) / 4;
+            const int GM = (G4 + kWave - 1) / kWave;
+            if constexpr (NW != kWaves) {  // GV: workgroup-wide single pass, else two passes
+              const int GT = (G4 + kWave * NW - 1) / (kWave * NW);
+              const int nh = k - 1;
+              if (!wide_history_pass(Pv, a.kcap, GV))
+                compact_products<GV ? 8 : 1, NW>(P, Pv, nh, SH, WH, hcoef, hrho, hc, gamma0, g, gp, hy_new, hg);
+              else if (GT <= 1) compact_products_wide<1, NW>(P, Pv, nh, SH, WH, hrho, hc, gamma0, g, gp, hy_new, hg, scratch, buf);
+              else if (GT == 2) compact_products_wide<2, NW>(P, Pv, nh, SH, WH, hrho, hc, gamma0, g, gp, hy_new, hg, scratch, buf);
+              else if (GT == 3) compact_products_wide<3, NW>(P, Pv, nh, SH, WH, hrho, hc, gamma0, g, gp, hy_new, hg, scratch, buf);
+              else if (GT == 4) compact_products_wide<4, NW>(P, Pv, nh, SH, WH, hrho, hc, gamma0, g, gp, hy_new, hg, scratch, buf);
+              else if (GT == 5) compact_products_wide<5, NW>(P, Pv, nh, SH, WH, hrho, hc, gamma0, g, gp, hy_new, hg, scratch, buf);
+              else if (GT == 6) compact_products_wide<6, NW>(P, Pv, nh, SH, WH, hrho, hc, gamma0, g, gp, hy_new, hg, scratch, buf);
+              else compact_products_wide<7, NW>(P, Pv, nh, SH, WH, hrho, hc, gamma0, g, gp, hy_new, hg, scratch, buf);
+            } else
+            if (GM <= 1) compact_products_fused<1>(P, Pv, k - 1, SH, WH, LH, lcap, hrho, hc, gamma0, g, gp, hy_new, hg, s_pend, hy_pend, d, hg);
+            else if (GM == 2) compact_products_fused<2>(P, Pv, k - 1, SH, WH, LH, lcap, hrho, hc, gamma0, g, gp, hy_new, hg, s_pend, hy_pend, d, hg);
+            else if (GM == 3) compact_products_fused<3>(P, Pv, k - 1, SH, WH, LH, lcap, hrho, hc, gamma0, g, gp, hy_new, hg, s_pend, hy_pend, d, hg);
+            else if (GM == 4) compact_products_fused<4>(P, Pv, k - 1, SH, WH, LH, lcap, hrho, hc, gamma0, g, gp, hy_new, hg, s_pend, hy_pend, d, hg);
+            else
+  #endif
+            // GV mode (very long rows, few resident waves): 8 column groups in flight per lane;
+            // the LDS-mode kernel keeps the lean loop (its register budget is the fused pass's)
+            compact_products<GV ? 8 : 1, NW>(P, Pv, k - 1, SH, WH, hcoef, hrho, hc, gamma0, g, gp, hy_new, hg);
+          }
+  #endif
+          __syncthreads();
+          DAVA_PHASE(1);
+          for (int i = tid; i < P; i += BLOCK) {
+            const float gi = g[i], yi = gi - gp[i], si = s_cur[i], hi = hy_new[i];
+            r[0] += si * yi; r[1] += hi * yi; r[2] += si * gi; r[3] += hi * gi;
+          }
+          block_sum<4, NW>(r, scratch, buf); buf ^= 1;
+          rho = r[0] <= 0.f ? 0.f : 1.0f / r[0];  // inverse_curvature (func_inverse_curvature.py:24-28)
+          c = 1.0f + rho * r[1];
+          sg = r[2];
+          hyg = r[3];
+        }
+        // d = -H_k g,  H_k = H' + c (rho s) s^T - (rho s) (H'y)^T - (H'y) (rho s)^T
+        const float rsg = rho * sg;
+        for (int i = tid; i < P; i += BLOCK) {
+          const float sri = s_cur[i] * rho;
+          d[i] = -1.0f * (hg[i] + sri * (c * sg) - sri * hyg - hy_new[i] * rsg);
+        }
+        if constexpr (MODE == DAVA_HESSIAN_DENSE) {
+          // the new update becomes the pending one; recycle the old buffers
+          { float* t = s_pend; s_pend = s_cur; s_cur = t; }
+          { float* t = hy_pend; hy_pend = hy_new; hy_new = t; }
+          pend_rho = rho;
+          pend_c = c;
+        } else if (k - 1 < a.kcap) {
+          // append U_k = (s, H y, rho, c) to the history (entry k-1), on-chip if it is one of the first lcap
+          if (k - 1 < lcap) {
+            float* sr = LH + (size_t)2 * (k - 1) * Pv;
+            for (int i = tid; i < Pv; i += BLOCK) { sr[i] = s_cur[i]; sr[Pv + i] = hy_new[i]; }
+          } else {
+            float* sr = SH + (size_t)(k - 1) * Pv;
+            float* wr = WH + (size_t)(k - 1) * Pv;
+            for (int i = tid; i < Pv; i += BLOCK) { sr[i] = s_cur[i]; wr[i] = hy_new[i]; }
+          }
+          if (tid == 0) { hrho[k - 1] = rho; hc[k - 1] = c; }
+        }
+        __syncthreads();
+      }
+
+      // ---- strong-Wolfe line search (wolfe_conditions.py:23-239) ----
+      float dphi0;
+      {
+        float r[1] = {0.f};
+        for (int i = tid; i < P; i += BLOCK) r[0] += d[i] * g[i];
+        block_sum<1, NW>(r, scratch, buf); buf ^= 1;
+        dphi0 = r[0];
+      }
+      DAVA_PHASE(2);
+      float a_lo = 0.f, a_hi = 0.f, al = 1.f, f_lo = E, f_hi = E, fa = E, dfa = dphi0;
+      float last_al = 0.f, last_fa = 0.f;
+      // Largest alpha seen whose trial point rounded back to x.  Rounding is monotone
+      // (0 <= a' <= a => |fl(a' d_i)| <= |fl(a d_i)| and fl(x_i + .) stays x_i), so every smaller
+      // trial is a no-move point too and needs neither evaluation nor the check: at fp32
+      // stagnation a bisection towards 0 runs ~150 such trials per line search (C2's slowest
+      // problems: thousands per solve).
+      float nomove_al = -1.0f;
+      bool widen = true, zoom = false, evaluated = false, last_same = false;
+      // trial gradients go into gp's buffer (g_prev is dead once d is formed)
+      const float lim = (-a.c2) * dphi0;
+      for (int t = 0; t < a.max_trials; ++t) {
+        if (!(widen || zoom)) break;
+        if (t > 0) {
+          if (widen) { a_hi = al; f_hi = fa; al = 2.0f * al; }
+          if (zoom) al = 0.5f * (a_lo + a_hi);
+        }
+        DAVA_PHASE(4);
+        // Trial points that round back to x exactly (tiny alpha, e.g. bisecting an uphill
+        // direction at fp32 stagnation) need no evaluation: the reference's closure would
+        // return f(x) and, via autograd w.r.t. alpha, (d * g).sum() -- exactly f0 and
+        // phi'(0).  The check rides on the objective's first reduction (CHECK).  Otherwise
+        // E and the full gradient at the trial point are formed (kept for reuse as the
+        // next iterate's gradient) and phi'(alpha) = d . grad (DOT).
+        const bool known_same = DAVA_TRIAL_CHECK && al <= nomove_al;  // uniform
+        if (!known_same &&
+            ba_eval<true, !DAVA_TRIAL_DOT, true, DAVA_TRIAL_DOT, DAVA_TRIAL_CHECK, RES, float, NW, PPT>(
+                L, x, d, al, obs, vis, grad_buf(gp), views, vpart, scratch, buf, fa, dfa)) {
+          ++evals;
+          last_same = false;
+        } else {
+          fa = E;
+          dfa = dphi0;
+          last_same = true;
+          if (!known_same) nomove_al = al;
+        }
+        DAVA_PHASE(3);
+        ++trials;
+        evaluated = true;
+        last_al = al;
+        last_fa = fa;
+        bool fail = fa > E + (a.c1 * al) * dphi0;
+        if (zoom) fail = fail || (fa >= f_lo);
+        if (t > 0 && widen) fail = fail || (fa >= f_hi);
+        const bool curv = a.strong ? (fabsf(dfa) <= lim) : (-1.0f * dfa <= lim);
+        const bool up = widen ? (dfa >= 0.f) : (dfa * (a_hi - a_lo) >= 0.f);
+        if (zoom) {
+          const bool done = !fail && curv;
+          const bool flip = !fail && !curv && up;
+          const bool setlo = !fail && !curv;
+          if (fail || done) { a_hi = al; f_hi = fa; }
+          if (flip) { a_hi = a_lo; f_hi = f_lo; }
+          if (setlo || done) { a_lo = al; f_lo = fa; }
+          if (done) zoom = false;
+        } else if (widen) {
+          const bool bracket = fail;
+          const bool done = !fail && curv;
+          const bool flip = !fail && !curv && up;
+          if (bracket) { a_lo = a_hi; f_lo = f_hi; }
+          if (bracket || done) { a_hi = al; f_hi = fa; }
+          if (done || flip) { a_lo = al; f_lo = fa; }
+          if (bracket || flip) zoom = true;
+          if (bracket || done || flip) widen = false;
+        }
+        if (a_lo == a_hi) zoom = false;
+      }
+      const float alpha = a_hi;
+      have_next = evaluated && last_al == alpha;
+      E_next = last_fa;
+      if (have_next && last_same) {  // x_{k+1} == x_k bitwise: its gradient is g itself
+        for (int i = tid; i < P; i += BLOCK) gp[i] = g[i];
+      } else if (have_next) {
+        publish(gp);  // XL: only the trial that is kept needs its gradient in the workspace
       }
       DAVA_PHASE(4);
-      // Trial points that round back to x exactly (tiny alpha, e.g. bisecting an uphill
-      // direction at fp32 stagnation) need no evaluation: the reference's closure would
-      // return f(x) and, via autograd w.r.t. alpha, (d * g).sum() -- exactly f0 and
-      // phi'(0).  The check rides on the objective's first reduction (CHECK).  Otherwise
-      // E and the full gradient at the trial point are formed (kept for reuse as the
-      // next iterate's gradient) and phi'(alpha) = d . grad (DOT).
-      const bool known_same = DAVA_TRIAL_CHECK && al <= nomove_al;  // uniform
-      if (!known_same &&
-          ba_eval<true, !DAVA_TRIAL_DOT, true, DAVA_TRIAL_DOT, DAVA_TRIAL_CHECK, RES, float, NW, PPT>(
-              L, x, d, al, obs, vis, grad_buf(gp), views, vpart, scratch, buf, fa, dfa)) {
-        ++evals;
-        last_same = false;
-      } else {
-        fa = E;
-        dfa = dphi0;
-        last_same = true;
-        if (!known_same) nomove_al = al;
-      }
-      DAVA_PHASE(3);
-      ++trials;
-      evaluated = true;
-      last_al = al;
-      last_fa = fa;
-      bool fail = fa > E + (a.c1 * al) * dphi0;
-      if (zoom) fail = fail || (fa >= f_lo);
-      if (t > 0 && widen) fail = fail || (fa >= f_hi);
-      const bool curv = a.strong ? (fabsf(dfa) <= lim) : (-1.0f * dfa <= lim);
-      const bool up = widen ? (dfa >= 0.f) : (dfa * (a_hi - a_lo) >= 0.f);
-      if (zoom) {
-        const bool done = !fail && curv;
-        const bool flip = !fail && !curv && up;
-        const bool setlo = !fail && !curv;
-        if (fail || done) { a_hi = al; f_hi = fa; }
-        if (flip) { a_hi = a_lo; f_hi = f_lo; }
-        if (setlo || done) { a_lo = al; f_lo = fa; }
-        if (done) zoom = false;
-      } else if (widen) {
-        const bool bracket = fail;
-        const bool done = !fail && curv;
-        const bool flip = !fail && !curv && up;
-        if (bracket) { a_lo = a_hi; f_lo = f_hi; }
-        if (bracket || done) { a_hi = al; f_hi = fa; }
-        if (done || flip) { a_lo = al; f_lo = fa; }
-        if (bracket || flip) zoom = true;
-        if (bracket || done || flip) widen = false;
-      }
-      if (a_lo == a_hi) zoom = false;
-    }
-    const float alpha = a_hi;
-    have_next = evaluated && last_al == alpha;
-    E_next = last_fa;
-    if (have_next && last_same) {  // x_{k+1} == x_k bitwise: its gradient is g itself
-      for (int i = tid; i < P; i += BLOCK) gp[i] = g[i];
-    } else if (have_next) {
-      publish(gp);  // XL: only the trial that is kept needs its gradient in the workspace
-    }
-    DAVA_PHASE(4);
 
-    // ---- take the step (bfgs_solver.py:191-199) and test its length (:203-207) ----
-    {
-      float r[1] = {0.f};
-      for (int i = tid; i < P; i += BLOCK) {
-        const float si = __fmul_rn(alpha, d[i]);
-        s_cur[i] = si;
-        x[i] = __fadd_rn(x[i], si);
-        r[0] += si * si;
+      // ---- take the step (bfgs_solver.py:191-199) and test its length (:203-207) ----
+      {
+        float r[1] = {0.f};
+        for (int i = tid; i < P; i += BLOCK) {
+          const float si = __fmul_rn(alpha, d[i]);
+          s_cur[i] = si;
+          x[i] = __fadd_rn(x[i], si);
+          r[0] += si * si;
+        }
+        block_sum<1, NW>(r, scratch, buf); buf ^= 1;
+        ++steps;
+        DAVA_PHASE(5);
+        if (!(sqrtf(r[0]) > a.min_step)) { reason = DAVA_STOP_STEP; break; }
       }
-      block_sum<1, NW>(r, scratch, buf); buf ^= 1;
-      ++steps;
-      DAVA_PHASE(5);
-      if (!(sqrtf(r[0]) > a.min_step)) { reason = DAVA_STOP_STEP; break; }
     }
-  }
-#if DAVA_PHASE_TIMING
-  ph_acc[kPhases - 1] = clock64() - ph_start;
-  if (tid == 0 && a.phase_cycles)
-    for (int i = 0; i < kPhases; ++i) a.phase_cycles[(size_t)b * kPhases + i] = ph_acc[i];
-#endif
+  #if DAVA_PHASE_TIMING
+    ph_acc[kPhases - 1] = clock64() - ph_start;
+    if (tid == 0 && a.phase_cycles)
+      for (int i = 0; i < kPhases; ++i) a.phase_cycles[(size_t)b * kPhases + i] = ph_acc[i];
+  #endif
 
-  // ---- outputs ----
-  __syncthreads();
-  float* xo = a.x_out + (size_t)b * P;
-  for (int i = tid; i < P; i += BLOCK) xo[i] = x[i];
-  if (a.err_out) {
-    float e2 = 0.f;
-    ba_eval<false, false, false, false, false, RES, float, NW, PPT>(L, x, nullptr, 0.f, obs, vis, nullptr, views, vpart, scratch, buf,
-                                                   e2, unused);
-    if (tid == 0) a.err_out[b] = e2;
-  }
-  if (a.status && tid == 0) {
-    int32_t* st = a.status + (size_t)b * DAVA_STATUS_WORDS;
-    st[0] = steps; st[1] = reason; st[2] = evals; st[3] = trials;
+    // ---- outputs ----
+    __syncthreads();
+    float* xo = a.x_out + (size_t)b * P;
+    for (int i = tid; i < P; i += BLOCK) xo[i] = x[i];
+    if (a.err_out) {
+      float e2 = 0.f;
+      ba_eval<false, false, false, false, false, RES, float, NW, PPT>(L, x, nullptr, 0.f, obs, vis, nullptr, views, vpart, scratch, buf,
+                                                     e2, unused);
+      if (tid == 0) a.err_out[b] = e2;
+    }
+    if (a.status && tid == 0) {
+      int32_t* st = a.status + (size_t)b * DAVA_STATUS_WORDS;
+      st[0] = steps; st[1] = reason; st[2] = evals; st[3] = trials;
+    }
+    if (!a.queue) break;
   }
 }
 
@@ -1017,13 +1031,20 @@ static int lds_history_entries(const DavaScene* s, int kcap, bool gv) {
 
 using namespace dava;
 
-extern "C" size_t dava_ba_solve_workspace_bytes(const DavaScene* scene, const DavaSolverConfig* config) {
-  if (check_scene(scene, false) != DAVA_OK || !config) return 0;
+// Bytes of the solve's state (vectors in GV mode + inverse-Hessian state); the work-queue
+// counter follows at that offset, in the last kQueueBytes of the workspace.
+constexpr size_t kQueueBytes = 256;
+static size_t solve_state_bytes(const DavaScene* scene, const DavaSolverConfig* config) {
   const int kcap = config->hessian_mode == DAVA_HESSIAN_COMPACT ? compact_capacity(config) : 0;
   const size_t vec = use_gv(scene, kcap) ? gv_vector_bytes(scene) : 0;
   if (config->hessian_mode == DAVA_HESSIAN_DENSE) return vec + dense_hessian_bytes(scene);
-  if (config->hessian_mode == DAVA_HESSIAN_COMPACT) return vec + compact_history_bytes(scene, config);
-  return 0;
+  return vec + compact_history_bytes(scene, config);
+}
+
+extern "C" size_t dava_ba_solve_workspace_bytes(const DavaScene* scene, const DavaSolverConfig* config) {
+  if (check_scene(scene, false) != DAVA_OK || !config) return 0;
+  if (config->hessian_mode != DAVA_HESSIAN_DENSE && config->hessian_mode != DAVA_HESSIAN_COMPACT) return 0;
+  return solve_state_bytes(scene, config) + kQueueBytes;
 }
 
 extern "C" int dava_ba_solve_plan(const DavaScene* scene, const DavaSolverConfig* config, DavaSolvePlan* plan) {
@@ -1044,10 +1065,31 @@ extern "C" int dava_ba_solve_plan(const DavaScene* scene, const DavaSolverConfig
 
 template <int MODE, bool GV, int RES, bool XL, int PPT>
 static void launch_solve_ppt(const SolveArgs& a, int B, int lds, hipStream_t s) {
+  const auto kernel = bfgs_ba_solve_kernel<MODE, GV, RES, XL, PPT>;
+  constexpr int threads = kWave * solve_waves(GV);
   if (lds > 64 * 1024)
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(bfgs_ba_solve_kernel<MODE, GV, RES, XL, PPT>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-  hipLaunchKernelGGL((bfgs_ba_solve_kernel<MODE, GV, RES, XL, PPT>), dim3(B), dim3(kWave * solve_waves(GV)), lds, s, a);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+  int grid = B;
+  SolveArgs args = a;
+  if (args.queue) {  // one workgroup per resident slot (host queries only; nothing synchronises)
+    int dev = 0, cus = 0, per_cu = 0;
+    if (hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, threads, lds) == hipSuccess && per_cu > 0 &&
+        cus > 0)
+      grid = min(B, per_cu * cus);
+    // The hardware already refills a slot as soon as its workgroup retires, but only from its
+    // own XCD's share of the grid (workgroups are dealt round-robin over the 8 XCDs): the
+    // queue pays where per-problem work is uneven -- stopping rules active, or few problems
+    // per slot so one long line search decides an XCD's finish (C2: +10%, C3 to convergence:
+    // +4.5%).  With fixed K and >= 8 problems per slot (C3: 16) it measured -1%: plain grid.
+    const bool fixed_k = !(args.thr >= 0.f) && !(args.min_step >= 0.f);
+    if (grid == B || (fixed_k && B >= 8 * grid)) {
+      args.queue = nullptr;
+      grid = B;
+    }
+  }
+  hipLaunchKernelGGL(kernel, dim3(grid), dim3(threads), lds, s, args);
 }
 
 // Points per thread held in registers by the objective: one for the LDS-mode kernels (C1-C3:
@@ -1090,9 +1132,12 @@ extern "C" int dava_ba_solve(const DavaScene* scene, const DavaSolverConfig* con
   const int lds = lds_bytes_for(scene, kcap, gv, lcap, xl);
   if (lds > kMaxLds) return DAVA_ERR_UNSUPPORTED;
   const size_t vec = gv ? gv_vector_bytes(scene) : 0;
-  const size_t need = vec + (mode == DAVA_HESSIAN_DENSE ? dense_hessian_bytes(scene) : compact_history_bytes(scene, config));
+  const size_t need = solve_state_bytes(scene, config);
   const bool uses_ws = gv || (mode == DAVA_HESSIAN_DENSE ? config->iterations > 2 : config->iterations > 1);
   if (uses_ws && (!workspace || workspace_bytes < need)) return DAVA_ERR_WORKSPACE;
+  // the work queue needs its counter in the workspace's tail (dava_ba_solve_workspace_bytes
+  // includes it); a workspace sized without it runs one workgroup per problem instead
+  const bool queue = workspace && workspace_bytes >= need + kQueueBytes && getenv("DAVA_NO_QUEUE") == nullptr;
   SolveArgs a;
   a.L = Layout{scene->num_views, scene->num_points, scene->num_parameters, scene->distortion ? 1 : 0};
   a.B = scene->batch;
@@ -1117,7 +1162,9 @@ extern "C" int dava_ba_solve(const DavaScene* scene, const DavaSolverConfig* con
   a.kcap = kcap;
   a.lcap = lcap;
   a.phase_cycles = nullptr;
+  a.queue = queue ? reinterpret_cast<int*>(static_cast<char*>(workspace) + need) : nullptr;
   hipStream_t s = static_cast<hipStream_t>(stream);
+  if (queue && hipMemsetAsync(a.queue, 0, sizeof(int), s) != hipSuccess) return DAVA_ERR_LAUNCH;
 #if DAVA_PHASE_TIMING
   const size_t ph_bytes = (size_t)scene->batch * kPhases * sizeof(unsigned long long);
   if (hipMalloc(&a.phase_cycles, ph_bytes) != hipSuccess) return DAVA_ERR_LAUNCH;

@@ -100,7 +100,12 @@ typedef struct DavaSolverConfig {
  * {steps taken, DavaStopReason, objective evaluations, line-search trials}. */
 #define DAVA_STATUS_WORDS 4
 
-/* Bytes of device workspace dava_ba_solve needs for this scene/config. */
+/* Bytes of device workspace dava_ba_solve needs for this scene/config: the solve's state
+ * (inverse-Hessian representation; O(P) vectors for large P) followed by a 256-byte
+ * work-queue counter.  A workspace of this size lets the launch run one workgroup per
+ * resident slot, each taking the next problem when it finishes one (problems that stop
+ * early free their slot); a workspace without the counter's 256 bytes still works, one
+ * workgroup per problem. */
 size_t dava_ba_solve_workspace_bytes(const DavaScene* scene, const DavaSolverConfig* config);
 
 /* How dava_ba_solve runs a scene/config (host-only query, no device needed): lets a caller

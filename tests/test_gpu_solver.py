@@ -265,6 +265,25 @@ def test_global_vector_mode_equals_lds_mode(device, mode, xl, monkeypatch):
     assert _rel(gv, lds).max() <= TOL
 
 
+@pytest.mark.parametrize("stopping", ["fixed", "reference"])
+def test_work_queue_launch_is_bitwise_invisible(device, stopping, monkeypatch):
+    """More problems than resident workgroups: with the work queue (a slot takes the next
+    problem when it finishes one) every problem's result and status are bitwise those of one
+    workgroup per problem (DAVA_NO_QUEUE).  2048 C1-shaped problems exceed the chip's slots,
+    and both the fixed-K and the reference stopping rules (problems retiring early) run."""
+    x0, obs, vis = _scene(2048, 2, 64, False, 559)
+    kw = dict(iterations=30, error_threshold=-1.0, minimum_step=-1.0) if stopping == "fixed" else dict(iterations=200)
+    out, st = _gpu_solve(device, x0, obs, vis, 2, 64, False, hessian_mode="compact", **kw)
+    monkeypatch.setenv("DAVA_NO_QUEUE", "1")
+    ref, st_ref = _gpu_solve(device, x0, obs, vis, 2, 64, False, hessian_mode="compact", **kw)
+    monkeypatch.delenv("DAVA_NO_QUEUE")
+    assert torch.equal(out, ref)
+    assert torch.equal(st, st_ref)
+    if stopping == "reference":
+        assert (st[:, 1] != 0).float().mean() > 0.5  # most problems stop by a rule, at different steps
+        assert st[:, 0].unique().numel() > 1
+
+
 @pytest.mark.parametrize("m,n,distortion", [(4, 256, True), (2, 128, False)])
 def test_lds_resident_history_is_bitwise_invisible(device, m, n, distortion, monkeypatch):
     """COMPACT mode keeps the oldest history entries on-chip (dava_ba_solve_plan); the products

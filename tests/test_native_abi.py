@@ -79,7 +79,8 @@ def test_workspace_size_dense(lib):
     from deep_attention_visual_odometry_amd import native_ops
 
     p = 3 + 3 * 256 + 6 * 3 + 5
-    assert native_ops.solve_workspace_bytes(8192, 4, 256, True) == 8192 * p * ((p + 31) // 32 * 32) * 4
+    # dense inverse Hessians + the 256-byte work-queue counter
+    assert native_ops.solve_workspace_bytes(8192, 4, 256, True) == 8192 * p * ((p + 31) // 32 * 32) * 4 + 256
 
 
 def test_solve_plan(lib, monkeypatch):
