@@ -669,10 +669,16 @@ __global__ __launch_bounds__(kWave * solve_waves(GV), DAVA_SOLVE_WAVES_PER_EU) v
       DAVA_PHASE(0);
       if (!(E > a.thr)) { reason = DAVA_STOP_ERROR; break; }
 
+      // phi'(0) = d . g is accumulated where d is formed (same per-thread order as a separate
+      // pass over d); its block reduction below is also the barrier that publishes d
+      float dg = 0.f;
       if (k == 0) {
         // first step: no inverse Hessian yet, d = -g (bfgs_solver.py:152-155)
-        for (int i = tid; i < P; i += BLOCK) d[i] = -1.0f * g[i];
-        __syncthreads();
+        for (int i = tid; i < P; i += BLOCK) {
+          const float di = -1.0f * g[i];
+          d[i] = di;
+          dg += di * g[i];
+        }
       } else {
         float r[4] = {0, 0, 0, 0};
         float rho, c, sg, hyg;
@@ -746,7 +752,9 @@ __global__ __launch_bounds__(kWave * solve_waves(GV), DAVA_SOLVE_WAVES_PER_EU) v
         const float rsg = rho * sg;
         for (int i = tid; i < P; i += BLOCK) {
           const float sri = s_cur[i] * rho;
-          d[i] = -1.0f * (hg[i] + sri * (c * sg) - sri * hyg - hy_new[i] * rsg);
+          const float di = -1.0f * (hg[i] + sri * (c * sg) - sri * hyg - hy_new[i] * rsg);
+          d[i] = di;
+          dg += di * g[i];
         }
         if constexpr (MODE == DAVA_HESSIAN_DENSE) {
           // the new update becomes the pending one; recycle the old buffers
@@ -766,14 +774,12 @@ __global__ __launch_bounds__(kWave * solve_waves(GV), DAVA_SOLVE_WAVES_PER_EU) v
           }
           if (tid == 0) { hrho[k - 1] = rho; hc[k - 1] = c; }
         }
-        __syncthreads();
       }
 
       // ---- strong-Wolfe line search (wolfe_conditions.py:23-239) ----
       float dphi0;
       {
-        float r[1] = {0.f};
-        for (int i = tid; i < P; i += BLOCK) r[0] += d[i] * g[i];
+        float r[1] = {dg};
         block_sum<1, NW>(r, scratch, buf); buf ^= 1;
         dphi0 = r[0];
       }
