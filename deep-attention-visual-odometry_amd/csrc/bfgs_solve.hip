@@ -438,6 +438,18 @@ __device__ __forceinline__ void compact_products_wide(int P, int Pv, int nh, con
 // Entries j < lcap are read from the LDS-resident history LH (S row at LH + 2 j Pv, W row
 // Pv floats later) -- the same values in the same per-wave order, so the result is
 // bitwise the same as with every entry in HBM.
+// Wave priorities (s_setprio): the two workgroups on a CU put one wave on each SIMD, and
+// VALU issue between them goes by priority, then age.  A wave streaming its history (HBM-
+// latency-bound, few VALU ops per byte) drops to 0 so the partner's objective evaluation or
+// line-search step (VALU/LDS-latency-bound, the critical path) issues first: C3 +1.0%
+// (interleaved A/B, profiles/r01c_ab_wave_priority.log; levels 1..3 within noise of
+// each other).  Equal values = never set.
+#ifndef DAVA_BASE_PRIO
+#define DAVA_BASE_PRIO 2
+#endif
+#ifndef DAVA_HIST_PRIO
+#define DAVA_HIST_PRIO 0
+#endif
 template <int GM>
 __device__ __forceinline__ void compact_products_fused(int P, int Pv, int nh, const float* __restrict__ S,
                                        const float* __restrict__ W, const float* LH, int lcap,
@@ -495,6 +507,9 @@ __device__ __forceinline__ void compact_products_fused(int P, int Pv, int nh, co
       w4[m] = ok[m] ? *reinterpret_cast<const f4v*>(wr + 4 * q) : f4v{0, 0, 0, 0};
     }
   };
+#if DAVA_HIST_PRIO != DAVA_BASE_PRIO
+  __builtin_amdgcn_s_setprio(DAVA_HIST_PRIO);
+#endif
   int j = wave;
   for (const int nl = min(lcap, nh); j < nl; j += kWaves) {  // on-chip entries first (wave-uniform)
     f4v s0[GM], w0[GM];
@@ -522,6 +537,9 @@ __device__ __forceinline__ void compact_products_fused(int P, int Pv, int nh, co
     load(j, s0, w0);
     consume(j, s0, w0);
   }
+#if DAVA_HIST_PRIO != DAVA_BASE_PRIO
+  __builtin_amdgcn_s_setprio(DAVA_BASE_PRIO);
+#endif
   // deterministic cross-wave sum: ((w0 + w2) + (w1 + w3)) + gamma0 * (y | g)
   auto put = [&](float* A, float* B) {
 #pragma unroll
@@ -567,6 +585,9 @@ __global__ __launch_bounds__(kWave * solve_waves(GV), DAVA_SOLVE_WAVES_PER_EU) v
   constexpr int NW = solve_waves(GV);
   constexpr int BLOCK = kWave * NW;
   extern __shared__ __attribute__((aligned(16))) float lds[];
+#if DAVA_BASE_PRIO
+  __builtin_amdgcn_s_setprio(DAVA_BASE_PRIO);
+#endif
   const Layout L = a.L;
   const int P = L.P, M = L.M, N = L.N;
   const int Pv = a.Pv;
