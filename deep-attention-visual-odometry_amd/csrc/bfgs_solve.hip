@@ -450,6 +450,9 @@ __device__ __forceinline__ void compact_products_wide(int P, int Pv, int nh, con
 #ifndef DAVA_HIST_PRIO
 #define DAVA_HIST_PRIO 0
 #endif
+#ifndef DAVA_DEFER_COMBINE
+#define DAVA_DEFER_COMBINE 1
+#endif
 template <int GM>
 __device__ __forceinline__ void compact_products_fused(int P, int Pv, int nh, const float* __restrict__ S,
                                        const float* __restrict__ W, const float* LH, int lcap,
@@ -562,6 +565,13 @@ __device__ __forceinline__ void compact_products_fused(int P, int Pv, int nh, co
   if (wave == 2) put(spare0, spare1);
   if (wave == 3) put(spare2, spare3);
   __syncthreads();
+  if (DAVA_DEFER_COMBINE) {
+    // leave (w0 + w2) in spare0/1 and (w1 + w3) in spare2/3: the caller's block-wide pass
+    // adds them and gamma0 (y | g) element by element (same operations, same order)
+    if (wave == 0) { add(spare0, spare1); put(spare0, spare1); }
+    if (wave == 1) { add(spare2, spare3); put(spare2, spare3); }
+    return;
+  }
   if (wave == 0) add(spare0, spare1);
   if (wave == 1) { add(spare2, spare3); put(spare2, spare3); }
   __syncthreads();
@@ -703,6 +713,7 @@ __global__ __launch_bounds__(kWave * solve_waves(GV), DAVA_SOLVE_WAVES_PER_EU) v
       } else {
         float r[4] = {0, 0, 0, 0};
         float rho, c, sg, hyg;
+        bool deferred = false;  // the fused pass left its last cross-wave add to the pass below
         if (k == 1) {
           // H_0 = gamma I, gamma from N&W eq. 6.20 (bfgs_solver.py:159-167, 217-233)
           for (int i = tid; i < P; i += BLOCK) {
@@ -733,6 +744,7 @@ __global__ __launch_bounds__(kWave * solve_waves(GV), DAVA_SOLVE_WAVES_PER_EU) v
   #ifndef DAVA_COMPACT_TWO_PASS
             const int G4 = (P + 3) / 4;
             const int GM = (G4 + kWave - 1) / kWave;
+            deferred = DAVA_DEFER_COMBINE && NW == kWaves && GM <= 4;
             if constexpr (NW != kWaves) {  // GV: workgroup-wide single pass, else two passes
               const int GT = (G4 + kWave * NW - 1) / (kWave * NW);
               const int nh = k - 1;
@@ -759,6 +771,17 @@ __global__ __launch_bounds__(kWave * solve_waves(GV), DAVA_SOLVE_WAVES_PER_EU) v
   #endif
           __syncthreads();
           DAVA_PHASE(1);
+          if (deferred) {  // finish the fused pass's cross-wave sum here, all threads at once
+            for (int i = tid; i < P; i += BLOCK) {
+              const float gi = g[i], yi = gi - gp[i], si = s_cur[i];
+              float hi = s_pend[i] + d[i], gh = hy_pend[i] + hg[i];
+              hi += gamma0 * yi;
+              gh += gamma0 * gi;
+              hy_new[i] = hi;
+              hg[i] = gh;
+              r[0] += si * yi; r[1] += hi * yi; r[2] += si * gi; r[3] += hi * gi;
+            }
+          } else
           for (int i = tid; i < P; i += BLOCK) {
             const float gi = g[i], yi = gi - gp[i], si = s_cur[i], hi = hy_new[i];
             r[0] += si * yi; r[1] += hi * yi; r[2] += si * gi; r[3] += hi * gi;
