@@ -10,5 +10,6 @@ tail -1 gpurun_out/final_smoke.log
 timeout -k 10 400 python3 bench.py > gpurun_out/final_bench.log 2>&1 || { tail -5 gpurun_out/final_bench.log; exit 1; }
 tail -1 gpurun_out/final_bench.log | cut -c1-300
 tools/measure_configs.sh || exit 1
-tools/profile.sh r01c_c3 > gpurun_out/prof_r01c.log 2>&1 || { tail -5 gpurun_out/prof_r01c.log; exit 1; }
-tail -1 gpurun_out/prof_r01c.log
+TAG=${1:-r01d}
+tools/profile.sh ${TAG}_c3 > gpurun_out/prof_$TAG.log 2>&1 || { tail -5 gpurun_out/prof_$TAG.log; exit 1; }
+tail -1 gpurun_out/prof_$TAG.log
