@@ -1,0 +1,455 @@
+"""The C ABI (include/dava_ba.h) registered as PyTorch operators: ``torch.ops.dava.*``.
+
+Every HIP entry point of ``libdava_ba.so`` is a ``torch.library`` custom op with a
+fake (meta) implementation, so ``torch.compile`` and FakeTensor tracing see opaque
+operators with known output shapes and dtypes (no graph break at a ctypes call),
+and eager calls dispatch straight to the HIP launch on the tensor's current stream.
+
+The ops are registered for the ``cuda`` (= ROCm/HIP) dispatch key only: a CPU tensor
+reaching one of them raises ``NotImplementedError`` from the dispatcher -- there is no
+CPU kernel and no fallback.  Outputs a caller did not ask for come back as empty
+(numel 0) tensors so every op has a fixed schema; ``native_ops`` maps them to None.
+Ops never alias or mutate their inputs, except the Wolfe state machine's
+``state``/``flags`` (declared in ``mutates_args``) and a caller-supplied workspace.
+"""
+from typing import Optional, Tuple
+
+import torch
+from torch import Tensor
+
+from . import _native as N
+
+_CUDA = "cuda"
+
+
+def _dt(t: Tensor) -> str:
+    if t.dtype == torch.float32:
+        return "f32"
+    if t.dtype == torch.float64:
+        return "f64"
+    raise TypeError(f"unsupported dtype {t.dtype}: the HIP kernels implement float32 and float64")
+
+
+def _empty0(like: Tensor, dtype=None) -> Tensor:
+    return like.new_empty((0,), dtype=dtype or like.dtype)
+
+
+def num_parameters(num_views: int, num_points: int, distortion: bool) -> int:
+    return 3 + 3 * num_points + 6 * (num_views - 1) + (5 if distortion else 0)
+
+
+def scene_struct(observations: Optional[Tensor], visibility: Optional[Tensor], num_views: int, num_points: int,
+                 distortion: bool, batch: int, residual: int = N.DAVA_RESIDUAL_SQUARED_REPROJECTION) -> N.DavaScene:
+    return N.DavaScene(batch, num_views, num_points, 1 if distortion else 0,
+                       num_parameters(num_views, num_points, distortion),
+                       N.ptr(observations), N.ptr(visibility), residual)
+
+
+def solver_config(sufficient_decrease, curvature, error_threshold, iterations, minimum_step, max_line_search_trials,
+                  strong, hessian_mode) -> N.DavaSolverConfig:
+    return N.DavaSolverConfig(float(sufficient_decrease), float(curvature), float(error_threshold),
+                              float(minimum_step), int(iterations), int(max_line_search_trials),
+                              1 if strong else 0, int(hessian_mode))
+
+
+def _check_scene_tensors(x: Tensor, observations: Tensor, visibility: Tensor, num_views: int, num_points: int,
+                         distortion: bool) -> None:
+    """Host-side shape checks BEFORE a launch: the kernels index with exactly these extents."""
+    b = x.shape[0]
+    p = num_parameters(num_views, num_points, distortion)
+    if x.dim() != 2 or x.shape[1] != p:
+        raise ValueError(f"parameters must be (B, {p}), got {tuple(x.shape)}")
+    if tuple(observations.shape) != (b, num_views, num_points, 2):
+        raise ValueError(f"observations must be ({b}, {num_views}, {num_points}, 2), got {tuple(observations.shape)}")
+    if tuple(visibility.shape) != (b, num_views, num_points):
+        raise ValueError(f"visibility must be ({b}, {num_views}, {num_points}), got {tuple(visibility.shape)}")
+    if observations.dtype != torch.float32 or visibility.dtype != torch.uint8:
+        raise TypeError("observations must be float32 and visibility uint8")
+    for t in (x, observations, visibility):
+        if not t.is_contiguous() or t.device != x.device:
+            raise ValueError("scene tensors must be contiguous and on one device")
+
+
+# ---------------------------------------------------------------- fused BA ops
+
+@torch.library.custom_op("dava::ba_solve", mutates_args=("workspace",), device_types=_CUDA)
+def ba_solve(x0: Tensor, observations: Tensor, visibility: Tensor, num_views: int, num_points: int,
+             distortion: bool, sufficient_decrease: float, curvature: float, error_threshold: float,
+             iterations: int, minimum_step: float, max_line_search_trials: int, strong: bool, hessian_mode: int,
+             residual: int, want_error: bool, workspace: Tensor) -> Tuple[Tensor, Tensor, Tensor]:
+    """``dava_ba_solve``: the whole eval-mode BFGS solve of a (B, P) fp32 batch in one launch.
+    ``workspace``: a uint8 scratch buffer of at least ``dava_ba_solve_workspace_bytes`` (its contents
+    are overwritten), or an empty tensor to allocate one per call.
+    Returns (x, error (B,) or empty, status (B, 4) int32)."""
+    lib = N.load_library()
+    _check_scene_tensors(x0, observations, visibility, num_views, num_points, distortion)
+    b = x0.shape[0]
+    dev = x0.device
+    sc = scene_struct(observations, visibility, num_views, num_points, distortion, b, residual)
+    cfg = solver_config(sufficient_decrease, curvature, error_threshold, iterations, minimum_step,
+                        max_line_search_trials, strong, hessian_mode)
+    need = int(lib.dava_ba_solve_workspace_bytes(sc, cfg))
+    if workspace.numel() < need or workspace.device != dev or workspace.dtype != torch.uint8:
+        if workspace.numel() > 0:
+            raise ValueError(f"workspace holds {workspace.numel()} bytes, the solve needs {need} (uint8, same device)")
+        workspace = torch.empty(max(need, 1), dtype=torch.uint8, device=dev)
+    x_out = torch.empty_like(x0)
+    err = torch.empty(b, device=dev, dtype=torch.float32) if want_error else _empty0(x0)
+    status = torch.empty((b, N.STATUS_WORDS), device=dev, dtype=torch.int32)
+    with torch.cuda.device(dev):
+        N.check(lib.dava_ba_solve(sc, cfg, N.ptr(x0), N.ptr(x_out), N.ptr(err) if want_error else None,
+                                  N.ptr(status), N.ptr(workspace), workspace.numel(), N.stream_of(dev)),
+                "dava_ba_solve")
+    return x_out, err, status
+
+
+@ba_solve.register_fake
+def _(x0, observations, visibility, num_views, num_points, distortion, sufficient_decrease, curvature,
+      error_threshold, iterations, minimum_step, max_line_search_trials, strong, hessian_mode, residual, want_error,
+      workspace):
+    b = x0.shape[0]
+    return (torch.empty_like(x0), x0.new_empty((b,) if want_error else (0,)),
+            x0.new_empty((b, N.STATUS_WORDS), dtype=torch.int32))
+
+
+@torch.library.custom_op("dava::ba_evaluate", mutates_args=(), device_types=_CUDA)
+def ba_evaluate(x: Tensor, observations: Tensor, visibility: Tensor, num_views: int, num_points: int,
+                distortion: bool, direction: Optional[Tensor], alpha: Optional[Tensor], want_grad: bool,
+                want_slope: bool, residual: int) -> Tuple[Tensor, Tensor, Tensor]:
+    """``dava_ba_evaluate``: E, dE/dx and d . dE/dx at x + alpha d.  Unrequested outputs are empty."""
+    lib = N.load_library()
+    _check_scene_tensors(x, observations, visibility, num_views, num_points, distortion)
+    b = x.shape[0]
+    for t in (direction, alpha):
+        if t is not None and (t.device != x.device or t.dtype != torch.float32 or not t.is_contiguous()):
+            raise ValueError("direction / alpha must be contiguous float32 on the parameters' device")
+    if direction is not None and direction.shape != x.shape:
+        raise ValueError("direction must have the parameters' shape")
+    if alpha is not None and alpha.numel() != b:
+        raise ValueError("alpha must hold one value per problem")
+    if want_slope and direction is None:
+        raise ValueError("the slope needs a direction")
+    err = torch.empty(b, device=x.device, dtype=torch.float32)
+    grad = torch.empty_like(x) if want_grad else _empty0(x)
+    slope = torch.empty(b, device=x.device, dtype=torch.float32) if want_slope else _empty0(x)
+    sc = scene_struct(observations, visibility, num_views, num_points, distortion, b, residual)
+    with torch.cuda.device(x.device):
+        N.check(lib.dava_ba_evaluate(sc, N.ptr(x), N.ptr(direction), N.ptr(alpha), N.ptr(err),
+                                     N.ptr(grad) if want_grad else None, N.ptr(slope) if want_slope else None,
+                                     N.stream_of(x.device)), "dava_ba_evaluate")
+    return err, grad, slope
+
+
+@ba_evaluate.register_fake
+def _(x, observations, visibility, num_views, num_points, distortion, direction, alpha, want_grad, want_slope,
+      residual):
+    b = x.shape[0]
+    return (x.new_empty((b,)), torch.empty_like(x) if want_grad else x.new_empty((0,)),
+            x.new_empty((b,) if want_slope else (0,)))
+
+
+@torch.library.custom_op("dava::ba_second_order", mutates_args=(), device_types=_CUDA)
+def ba_second_order(x: Tensor, observations: Tensor, visibility: Tensor, num_views: int, num_points: int,
+                    distortion: bool, direction: Optional[Tensor], residual: int, want_hv: bool,
+                    want_obs: bool) -> Tuple[Tensor, Tensor, Tensor, Tensor, Tensor]:
+    """``dava_ba_second_order``: (E, dE/dx, H v, dE/dobs, (d2E/dobs dx) v), forward-over-reverse.
+    direction None means v = 0.  Unrequested outputs are empty."""
+    lib = N.load_library()
+    _check_scene_tensors(x, observations, visibility, num_views, num_points, distortion)
+    if direction is not None and (direction.shape != x.shape or direction.dtype != torch.float32
+                                  or not direction.is_contiguous()):
+        raise ValueError("direction must be a contiguous float32 tensor of the parameters' shape")
+    b = x.shape[0]
+    err = torch.empty(b, device=x.device, dtype=torch.float32)
+    grad = torch.empty_like(x)
+    hv = torch.empty_like(x) if want_hv else _empty0(x)
+    obs_grad = torch.empty_like(observations) if want_obs else _empty0(x)
+    obs_hv = torch.empty_like(observations) if (want_obs and want_hv) else _empty0(x)
+    sc = scene_struct(observations, visibility, num_views, num_points, distortion, b, residual)
+    with torch.cuda.device(x.device):
+        N.check(lib.dava_ba_second_order(sc, N.ptr(x), N.ptr(direction), N.ptr(err), N.ptr(grad),
+                                         N.ptr(hv) if want_hv else None, N.ptr(obs_grad) if want_obs else None,
+                                         N.ptr(obs_hv) if (want_obs and want_hv) else None, N.stream_of(x.device)),
+                "dava_ba_second_order")
+    return err, grad, hv, obs_grad, obs_hv
+
+
+@ba_second_order.register_fake
+def _(x, observations, visibility, num_views, num_points, distortion, direction, residual, want_hv, want_obs):
+    b = x.shape[0]
+    return (x.new_empty((b,)), torch.empty_like(x), torch.empty_like(x) if want_hv else x.new_empty((0,)),
+            torch.empty_like(observations) if want_obs else x.new_empty((0,)),
+            torch.empty_like(observations) if (want_obs and want_hv) else x.new_empty((0,)))
+
+
+# ------------------------------------------------- generic BFGS building blocks
+
+def _square_batch(h: Tensor) -> Tuple[int, int]:
+    if h.dim() != 3 or h.shape[1] != h.shape[2]:
+        raise ValueError(f"expected a (B, n, n) batch of matrices, got {tuple(h.shape)}")
+    return h.shape[0], h.shape[1]
+
+
+def _same(t: Tensor, like: Tensor, shape, what: str) -> None:
+    if tuple(t.shape) != tuple(shape) or t.dtype != like.dtype or t.device != like.device or not t.is_contiguous():
+        raise ValueError(f"{what}: expected contiguous {like.dtype} {tuple(shape)} on {like.device}, "
+                         f"got {t.dtype} {tuple(t.shape)} on {t.device}")
+
+
+@torch.library.custom_op("dava::bfgs_update_inverse_hessian", mutates_args=(), device_types=_CUDA)
+def bfgs_update_inverse_hessian(h: Tensor, s: Tensor, y: Tensor) -> Tensor:
+    """(B, n, n), (B, n), (B, n) -> H+ (``bfgs_solver.py:235-303``)."""
+    b, n = _square_batch(h)
+    _same(s, h, (b, n), "step")
+    _same(y, h, (b, n), "delta_gradient")
+    out = torch.empty_like(h)
+    with torch.cuda.device(h.device):
+        N.check(getattr(N.load_library(), f"dava_bfgs_update_inverse_hessian_{_dt(h)}")(
+            b, n, N.ptr(h), N.ptr(s), N.ptr(y), N.ptr(out), N.stream_of(h.device)), "dava_bfgs_update_inverse_hessian")
+    return out
+
+
+@bfgs_update_inverse_hessian.register_fake
+def _(h, s, y):
+    return torch.empty_like(h)
+
+
+@torch.library.custom_op("dava::bfgs_update_inverse_hessian_backward", mutates_args=(), device_types=_CUDA)
+def bfgs_update_inverse_hessian_backward(h: Tensor, s: Tensor, y: Tensor, grad: Tensor, need_h: bool, need_s: bool,
+                                         need_y: bool) -> Tuple[Tensor, Tensor, Tensor]:
+    b, n = _square_batch(h)
+    _same(grad, h, (b, n, n), "grad")
+    gh = torch.empty_like(h) if need_h else _empty0(h)
+    gs = torch.empty_like(s) if need_s else _empty0(h)
+    gy = torch.empty_like(y) if need_y else _empty0(h)
+    with torch.cuda.device(h.device):
+        N.check(getattr(N.load_library(), f"dava_bfgs_update_inverse_hessian_backward_{_dt(h)}")(
+            b, n, N.ptr(h), N.ptr(s), N.ptr(y), N.ptr(grad), N.ptr(gh) if need_h else None,
+            N.ptr(gs) if need_s else None, N.ptr(gy) if need_y else None, N.stream_of(h.device)),
+            "dava_bfgs_update_inverse_hessian_backward")
+    return gh, gs, gy
+
+
+@bfgs_update_inverse_hessian_backward.register_fake
+def _(h, s, y, grad, need_h, need_s, need_y):
+    return (torch.empty_like(h) if need_h else h.new_empty((0,)), torch.empty_like(s) if need_s else h.new_empty((0,)),
+            torch.empty_like(y) if need_y else h.new_empty((0,)))
+
+
+@torch.library.custom_op("dava::bfgs_initial_scale", mutates_args=(), device_types=_CUDA)
+def bfgs_initial_scale(s: Tensor, y: Tensor) -> Tensor:
+    """(B, n), (B, n) -> gamma (B,) (``bfgs_solver.py:217-233``)."""
+    b, n = s.shape
+    _same(y, s, (b, n), "delta_gradient")
+    out = s.new_empty((b,))
+    with torch.cuda.device(s.device):
+        N.check(getattr(N.load_library(), f"dava_bfgs_initial_scale_{_dt(s)}")(
+            b, n, N.ptr(s), N.ptr(y), N.ptr(out), N.stream_of(s.device)), "dava_bfgs_initial_scale")
+    return out
+
+
+@bfgs_initial_scale.register_fake
+def _(s, y):
+    return s.new_empty((s.shape[0],))
+
+
+@torch.library.custom_op("dava::bfgs_initial_scale_backward", mutates_args=(), device_types=_CUDA)
+def bfgs_initial_scale_backward(s: Tensor, y: Tensor, grad: Tensor, need_s: bool,
+                                need_y: bool) -> Tuple[Tensor, Tensor]:
+    b, n = s.shape
+    _same(grad, s, (b,), "grad")
+    gs = torch.empty_like(s) if need_s else _empty0(s)
+    gy = torch.empty_like(y) if need_y else _empty0(s)
+    with torch.cuda.device(s.device):
+        N.check(getattr(N.load_library(), f"dava_bfgs_initial_scale_backward_{_dt(s)}")(
+            b, n, N.ptr(s), N.ptr(y), N.ptr(grad), N.ptr(gs) if need_s else None, N.ptr(gy) if need_y else None,
+            N.stream_of(s.device)), "dava_bfgs_initial_scale_backward")
+    return gs, gy
+
+
+@bfgs_initial_scale_backward.register_fake
+def _(s, y, grad, need_s, need_y):
+    return (torch.empty_like(s) if need_s else s.new_empty((0,)), torch.empty_like(y) if need_y else s.new_empty((0,)))
+
+
+@torch.library.custom_op("dava::bfgs_scale_matrix", mutates_args=(), device_types=_CUDA)
+def bfgs_scale_matrix(scale: Tensor, h: Tensor) -> Tensor:
+    """scale (B,) * H (B, n, n): the k == 1 rescale of H0 (``bfgs_solver.py:159-167``)."""
+    b, n = _square_batch(h)
+    _same(scale, h, (b,), "scale")
+    out = torch.empty_like(h)
+    with torch.cuda.device(h.device):
+        N.check(getattr(N.load_library(), f"dava_bfgs_scale_matrix_{_dt(h)}")(
+            b, n, N.ptr(scale), N.ptr(h), N.ptr(out), N.stream_of(h.device)), "dava_bfgs_scale_matrix")
+    return out
+
+
+@bfgs_scale_matrix.register_fake
+def _(scale, h):
+    return torch.empty_like(h)
+
+
+@torch.library.custom_op("dava::bfgs_scale_matrix_backward", mutates_args=(), device_types=_CUDA)
+def bfgs_scale_matrix_backward(scale: Tensor, h: Tensor, grad: Tensor, need_scale: bool,
+                               need_h: bool) -> Tuple[Tensor, Tensor]:
+    b, n = _square_batch(h)
+    _same(grad, h, (b, n, n), "grad")
+    gsc = torch.empty_like(scale) if need_scale else _empty0(h)
+    gh = torch.empty_like(h) if need_h else _empty0(h)
+    with torch.cuda.device(h.device):
+        N.check(getattr(N.load_library(), f"dava_bfgs_scale_matrix_backward_{_dt(h)}")(
+            b, n, N.ptr(scale), N.ptr(h), N.ptr(grad), N.ptr(gsc) if need_scale else None,
+            N.ptr(gh) if need_h else None, N.stream_of(h.device)), "dava_bfgs_scale_matrix_backward")
+    return gsc, gh
+
+
+@bfgs_scale_matrix_backward.register_fake
+def _(scale, h, grad, need_scale, need_h):
+    return (torch.empty_like(scale) if need_scale else h.new_empty((0,)),
+            torch.empty_like(h) if need_h else h.new_empty((0,)))
+
+
+@torch.library.custom_op("dava::bfgs_search_direction", mutates_args=(), device_types=_CUDA)
+def bfgs_search_direction(h: Tensor, g: Tensor) -> Tensor:
+    """d = -H g (``bfgs_solver.py:173-176``)."""
+    b, n = _square_batch(h)
+    _same(g, h, (b, n), "gradient")
+    out = torch.empty_like(g)
+    with torch.cuda.device(h.device):
+        N.check(getattr(N.load_library(), f"dava_bfgs_search_direction_{_dt(h)}")(
+            b, n, N.ptr(h), N.ptr(g), N.ptr(out), N.stream_of(h.device)), "dava_bfgs_search_direction")
+    return out
+
+
+@bfgs_search_direction.register_fake
+def _(h, g):
+    return torch.empty_like(g)
+
+
+@torch.library.custom_op("dava::bfgs_search_direction_backward", mutates_args=(), device_types=_CUDA)
+def bfgs_search_direction_backward(h: Tensor, g: Tensor, grad: Tensor, need_h: bool,
+                                   need_g: bool) -> Tuple[Tensor, Tensor]:
+    b, n = _square_batch(h)
+    _same(grad, h, (b, n), "grad")
+    gh = torch.empty_like(h) if need_h else _empty0(h)
+    gg = torch.empty_like(g) if need_g else _empty0(h)
+    with torch.cuda.device(h.device):
+        N.check(getattr(N.load_library(), f"dava_bfgs_search_direction_backward_{_dt(h)}")(
+            b, n, N.ptr(h), N.ptr(g), N.ptr(grad), N.ptr(gh) if need_h else None, N.ptr(gg) if need_g else None,
+            N.stream_of(h.device)), "dava_bfgs_search_direction_backward")
+    return gh, gg
+
+
+@bfgs_search_direction_backward.register_fake
+def _(h, g, grad, need_h, need_g):
+    return (torch.empty_like(h) if need_h else h.new_empty((0,)), torch.empty_like(g) if need_g else h.new_empty((0,)))
+
+
+# ------------------------------------------------------- batched Wolfe state machine
+
+WOLFE_STATE_COLUMNS = 9
+WOLFE_FLAG_COLUMNS = 2
+
+
+@torch.library.custom_op("dava::wolfe_init", mutates_args=(), device_types=_CUDA)
+def wolfe_init(direction: Tensor, f0: Tensor, g0: Tensor) -> Tuple[Tensor, Tensor]:
+    """(state (B, 9), flags (B, 2) uint8) for a line search along ``direction`` from (f0, g0)."""
+    b, n = direction.shape
+    _same(g0, direction, (b, n), "base_gradient")
+    _same(f0, direction, (b,), "base_error")
+    state = direction.new_empty((b, WOLFE_STATE_COLUMNS))
+    flags = direction.new_empty((b, WOLFE_FLAG_COLUMNS), dtype=torch.uint8)
+    with torch.cuda.device(direction.device):
+        N.check(getattr(N.load_library(), f"dava_wolfe_init_{_dt(direction)}")(
+            b, n, N.ptr(direction), N.ptr(f0), N.ptr(g0), N.ptr(state), N.ptr(flags), N.stream_of(direction.device)),
+            "dava_wolfe_init")
+    return state, flags
+
+
+@wolfe_init.register_fake
+def _(direction, f0, g0):
+    b = direction.shape[0]
+    return direction.new_empty((b, WOLFE_STATE_COLUMNS)), direction.new_empty((b, WOLFE_FLAG_COLUMNS),
+                                                                               dtype=torch.uint8)
+
+
+def _check_wolfe(state: Tensor, flags: Tensor) -> int:
+    b = state.shape[0]
+    if tuple(state.shape) != (b, WOLFE_STATE_COLUMNS) or tuple(flags.shape) != (b, WOLFE_FLAG_COLUMNS) \
+            or flags.dtype != torch.uint8 or not state.is_contiguous() or not flags.is_contiguous():
+        raise ValueError("Wolfe state must be (B, 9) and flags (B, 2) uint8, contiguous")
+    return b
+
+
+@torch.library.custom_op("dava::wolfe_propose", mutates_args=("state",), device_types=_CUDA)
+def wolfe_propose(state: Tensor, flags: Tensor) -> None:
+    """Next trial alpha of every active line search (widen x2 or bisect), in place."""
+    b = _check_wolfe(state, flags)
+    with torch.cuda.device(state.device):
+        N.check(getattr(N.load_library(), f"dava_wolfe_propose_{_dt(state)}")(
+            b, N.ptr(state), N.ptr(flags), N.stream_of(state.device)), "dava_wolfe_propose")
+
+
+@wolfe_propose.register_fake
+def _(state, flags):
+    return None
+
+
+@torch.library.custom_op("dava::wolfe_update", mutates_args=("state", "flags"), device_types=_CUDA)
+def wolfe_update(state: Tensor, flags: Tensor, trial: int, c1: float, c2: float, strong: bool) -> None:
+    """Consume (f(alpha), phi'(alpha)) already written into ``state`` and advance the brackets."""
+    b = _check_wolfe(state, flags)
+    with torch.cuda.device(state.device):
+        N.check(getattr(N.load_library(), f"dava_wolfe_update_{_dt(state)}")(
+            b, int(trial), float(c1), float(c2), 1 if strong else 0, N.ptr(state), N.ptr(flags),
+            N.stream_of(state.device)), "dava_wolfe_update")
+
+
+@wolfe_update.register_fake
+def _(state, flags, trial, c1, c2, strong):
+    return None
+
+
+# ------------------------------------------------ legacy L1 camera model evaluation
+
+@torch.library.custom_op("dava::l1_camera_evaluate", mutates_args=(), device_types=_CUDA)
+def l1_camera_evaluate(focal: Tensor, cx: Tensor, cy: Tensor, translation: Tensor, lie: Tensor, world: Tensor,
+                       target: Tensor, visibility: Tensor, minimum_z_distance: float, maximum_pixel_ratio: float,
+                       max_gradient: float, error_scale: float, want_error: bool,
+                       want_gradient: bool) -> Tuple[Tensor, Tensor]:
+    """``dava_l1_camera_evaluate``: PinholeCameraModelL1 error (B, E) and its hand-written gradient
+    (B, E, P) (``camera_model/pinhole_camera_model_l1.py:132-285``).  Shapes: focal/cx/cy (B, E),
+    translation/lie (B, E, M, 3), world (B, E, N-2, 3), target (B, M, N, 2), visibility (B, M, N) uint8."""
+    b, e = focal.shape
+    m, n = target.shape[1], target.shape[2]
+    p = 3 + 6 * m + 3 * n - 7
+    for t, shape, what in ((cx, (b, e), "cx"), (cy, (b, e), "cy"), (translation, (b, e, m, 3), "translation"),
+                           (lie, (b, e, m, 3), "orientation"), (world, (b, e, n - 2, 3), "world_points"),
+                           (target, (b, m, n, 2), "true_projected_points")):
+        _same(t, focal, shape, what)
+    if tuple(visibility.shape) != (b, m, n) or visibility.dtype != torch.uint8 or not visibility.is_contiguous():
+        raise ValueError("visibility must be a contiguous (B, M, N) uint8 tensor")
+    err = focal.new_empty((b, e)) if want_error else _empty0(focal)
+    grad = focal.new_empty((b, e, p)) if want_gradient else _empty0(focal)
+    with torch.cuda.device(focal.device):
+        N.check(getattr(N.load_library(), f"dava_l1_camera_evaluate_{_dt(focal)}")(
+            b, e, m, n, N.ptr(focal), N.ptr(cx), N.ptr(cy), N.ptr(translation), N.ptr(lie), N.ptr(world),
+            N.ptr(target), N.ptr(visibility), minimum_z_distance, maximum_pixel_ratio, max_gradient, error_scale,
+            N.ptr(err) if want_error else None, N.ptr(grad) if want_gradient else None, N.stream_of(focal.device)),
+            "dava_l1_camera_evaluate")
+    return err, grad
+
+
+@l1_camera_evaluate.register_fake
+def _(focal, cx, cy, translation, lie, world, target, visibility, minimum_z_distance, maximum_pixel_ratio,
+      max_gradient, error_scale, want_error, want_gradient):
+    b, e = focal.shape
+    m, n = target.shape[1], target.shape[2]
+    return (focal.new_empty((b, e) if want_error else (0,)),
+            focal.new_empty((b, e, 3 + 6 * m + 3 * n - 7) if want_gradient else (0,)))
+
+
+OPS = ("ba_solve", "ba_evaluate", "ba_second_order", "bfgs_update_inverse_hessian",
+       "bfgs_update_inverse_hessian_backward", "bfgs_initial_scale", "bfgs_initial_scale_backward",
+       "bfgs_scale_matrix", "bfgs_scale_matrix_backward", "bfgs_search_direction", "bfgs_search_direction_backward",
+       "wolfe_init", "wolfe_propose", "wolfe_update", "l1_camera_evaluate")

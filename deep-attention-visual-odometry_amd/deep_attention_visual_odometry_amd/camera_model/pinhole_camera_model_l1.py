@@ -20,9 +20,10 @@ from typing import Optional
 import torch
 
 from .. import _native as N
+from .. import _ops  # noqa: F401  (registers torch.ops.dava.l1_camera_evaluate)
 from ..geometry.lie_rotation import LieRotation
 from ..solvers.i_optimisable_function import IOptimisableFunction
-from ..utils import masked_merge_tensors
+from ..utils import merge_cached_values
 
 
 def _c(t: torch.Tensor) -> torch.Tensor:
@@ -114,7 +115,6 @@ class PinholeCameraModelL1(IOptimisableFunction):
 
     # ---- evaluation (HIP) ----
     def _evaluate(self, want_error: bool, want_gradient: bool):
-        lib = N.load_library()
         N.require_device_tensor(self._focal_length, "focal_length")
         inputs = (self._focal_length, self._cx, self._cy, self._translation, self._orientation.lie_vector,
                   self._world_points)
@@ -129,7 +129,6 @@ class PinholeCameraModelL1(IOptimisableFunction):
             dt = torch.get_default_dtype()
         if dt not in (torch.float32, torch.float64):
             raise TypeError("PinholeCameraModelL1 evaluates in float32 or float64")
-        suffix = "f32" if dt == torch.float32 else "f64"
         b, e, m, n = self.batch_size, self.num_estimates, self._num_views, self._num_points
         dev = self.device
         cast = lambda t: _c(t.detach().to(device=dev, dtype=dt))  # noqa: E731
@@ -141,14 +140,12 @@ class PinholeCameraModelL1(IOptimisableFunction):
         world = cast(self._world_points).reshape(b, e, n - 2, 3)
         target = cast(self._true_projected_points).reshape(b, m, n, 2)
         vis = _c(self._visibility_mask.detach().to(device=dev, dtype=torch.uint8)).reshape(b, m, n)
-        err = torch.empty(b, e, device=dev, dtype=dt) if want_error else None
-        grad = torch.empty(b, e, self.num_parameters, device=dev, dtype=dt) if want_gradient else None
-        with torch.cuda.device(dev):
-            N.check(getattr(lib, f"dava_l1_camera_evaluate_{suffix}")(
-                b, e, m, n, N.ptr(focal), N.ptr(cx), N.ptr(cy), N.ptr(trans), N.ptr(lie), N.ptr(world),
-                N.ptr(target), N.ptr(vis), self.minimum_z_distance, self.maximum_pixel_ratio, self._max_gradient,
-                float(self._error_scale.item()), N.ptr(err), N.ptr(grad), N.stream_of(dev)),
-                "dava_l1_camera_evaluate")
+        err, grad = torch.ops.dava.l1_camera_evaluate(
+            focal, cx, cy, trans, lie, world, target, vis, float(self.minimum_z_distance),
+            float(self.maximum_pixel_ratio), float(self._max_gradient), float(self._error_scale.item()),
+            bool(want_error), bool(want_gradient))
+        err = err if want_error else None
+        grad = grad if want_gradient else None
         return err, grad
 
     def get_error(self) -> torch.Tensor:
@@ -233,8 +230,8 @@ class PinholeCameraModelL1(IOptimisableFunction):
         else:
             world_mask = mask[:, :, None, None].tile(1, 1, *self._world_points.shape[2:])
             world_points = torch.where(world_mask, other._world_points, self._world_points)
-        error, error_mask = masked_merge_tensors(self._error, self._error_mask, other._error, other._error_mask, mask)
-        gradient, gradient_mask = masked_merge_tensors(self._gradient, self._gradient_mask, other._gradient,
+        error, error_mask = merge_cached_values(self._error, self._error_mask, other._error, other._error_mask, mask)
+        gradient, gradient_mask = merge_cached_values(self._gradient, self._gradient_mask, other._gradient,
                                                        other._gradient_mask, mask)
         return type(self)(
             focal_length=focal, cx=cx, cy=cy, translation=translation, orientation=orientation,

@@ -52,9 +52,24 @@ def gather_rows(local: torch.Tensor, global_batch: int, group: Optional[dist.Pro
     return torch.cat([buf[r * width: r * width + sizes[r]] for r in range(world)])
 
 
+def gather_packed(x: torch.Tensor, status: torch.Tensor, global_batch: int,
+                  group: Optional[dist.ProcessGroup] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+    """ONE all-gather for a solve's outputs: x (n, P) float32 and status (n, S) int32 travel
+    as one (n, P + S) float32 buffer (status bit-cast, not converted), split again after."""
+    if x.dtype != torch.float32 or status.dtype != torch.int32:
+        raise TypeError("gather_packed expects float32 parameters and int32 status words")
+    p = x.shape[-1]
+    packed = torch.cat([x.reshape(x.shape[0], p), status.reshape(status.shape[0], -1).view(torch.float32)], dim=1)
+    out = gather_rows(packed, global_batch, group)
+    return out[:, :p].contiguous(), out[:, p:].contiguous().view(torch.int32)
+
+
 def solve_sharded(solve_slab: Callable[[Shard], Tuple[torch.Tensor, torch.Tensor]], global_batch: int,
                   group: Optional[dist.ProcessGroup] = None) -> Tuple[torch.Tensor, torch.Tensor]:
-    """Run ``solve_slab(shard) -> (x (n, P), status (n, 4))`` on this rank's slab, then all-gather both."""
+    """Run ``solve_slab(shard) -> (x (n, P), status (n, 4))`` on this rank's slab, then all-gather
+    both in one collective (float32 parameters) or two (other dtypes)."""
     shard = shard_range(global_batch, dist.get_world_size(group), dist.get_rank(group))
     x, status = solve_slab(shard)
+    if x.dtype == torch.float32 and status.dtype == torch.int32:
+        return gather_packed(x, status, global_batch, group)
     return gather_rows(x, global_batch, group), gather_rows(status, global_batch, group)

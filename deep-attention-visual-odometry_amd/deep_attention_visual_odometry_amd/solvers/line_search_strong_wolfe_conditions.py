@@ -15,7 +15,7 @@ import warnings
 import torch
 import torch.nn as nn
 
-from ..utils import interpolate_alpha
+from ..utils import secant_alpha
 from .i_optimisable_function import IOptimisableFunction
 
 
@@ -82,7 +82,7 @@ class LineSearchStrongWolfeConditions(nn.Module):
 
         # ---- zoom (N&W 3.6) with secant interpolation of the slopes ----
         for _ in range(self.zoom_iterations):
-            alpha = interpolate_alpha(a_lo[zoom], a_hi[zoom], slope(fn_lo, zoom), slope(fn_hi, zoom))
+            alpha = secant_alpha(a_lo[zoom], a_hi[zoom], slope(fn_lo, zoom), slope(fn_hi, zoom))
             alpha_full = torch.zeros_like(a_hi)
             alpha_full[zoom] = alpha
             trial_step = torch.zeros_like(d)

@@ -1,54 +1,52 @@
-"""Small tensor utilities of the legacy solver path (``utils/masked_merge.py``,
-``utils/func_interpolate_alpha.py``)."""
+"""Bookkeeping helpers of the legacy ``IOptimisableFunction`` path (host-side tensor plumbing, no math
+on the hot path).  Behaviour follows the reference's ``utils/masked_merge.py:4-60`` and
+``utils/func_interpolate_alpha.py``; the formulation here is this project's own."""
 from typing import Optional, Tuple
 
 import torch
 
 
-def masked_merge_tensors(
+def merge_cached_values(
     values_1: Optional[torch.Tensor],
-    mask_1: Optional[torch.Tensor],
+    valid_1: Optional[torch.Tensor],
     values_2: Optional[torch.Tensor],
-    mask_2: Optional[torch.Tensor],
-    update_mask: torch.Tensor,
+    valid_2: Optional[torch.Tensor],
+    take_second: torch.Tensor,
 ) -> Tuple[Optional[torch.Tensor], Optional[torch.Tensor]]:
-    """Values from 1 where ``update_mask`` is false, from 2 where true, with the merged
-    validity mask (None = all valid), exactly as ``utils/masked_merge.py``."""
+    """Merge two per-estimate caches (e.g. a function's error or gradient) by selector.
+
+    Each cache is ``(values, valid)``: ``values`` None = nothing cached; ``valid`` None = every
+    cached row is valid, else a bool tensor over the leading (selector-shaped) dimensions.  Row
+    ``i`` of the result comes from cache 2 where ``take_second[i]`` and from cache 1 elsewhere, and
+    is valid iff the row it came from was.  A side with no values contributes no valid rows, and
+    the result's values are then the other side's tensor as-is.  Returns ``(values, valid)``,
+    ``valid`` None when every row is valid because both sides were fully valid."""
     if values_1 is None and values_2 is None:
         return None, None
-    if values_1 is not None and values_2 is not None:
-        vmask = update_mask
-        if update_mask.ndim < values_1.ndim:
-            vmask = update_mask.reshape(*update_mask.shape, *(1 for _ in range(values_1.ndim - update_mask.ndim)))
-            vmask = vmask.tile(*(1 for _ in range(update_mask.ndim)), *values_1.shape[update_mask.ndim:])
-        merged = torch.where(vmask, values_2, values_1)
-        if mask_1 is None and mask_2 is None:
-            return merged, None
-        if mask_1 is not None and mask_2 is not None:
-            return merged, torch.where(update_mask, mask_2, mask_1)
-        if mask_1 is not None:
-            return merged, torch.logical_or(mask_1, update_mask)
-        return merged, torch.logical_or(mask_2, torch.logical_not(update_mask))
-    if values_1 is not None:
-        if mask_1 is not None:
-            return values_1, torch.logical_and(mask_1, torch.logical_not(update_mask))
-        return values_1, torch.logical_not(update_mask)
-    if mask_2 is not None:
-        return values_2, torch.logical_and(mask_2, update_mask)
-    return values_2, update_mask
+    if values_1 is None or values_2 is None:
+        present_is_2 = values_1 is None
+        values = values_2 if present_is_2 else values_1
+        own = valid_2 if present_is_2 else valid_1
+        rows = take_second if present_is_2 else ~take_second
+        return values, (rows if own is None else own & rows)
+    selector = take_second.reshape(take_second.shape + (1,) * (values_1.ndim - take_second.ndim))
+    values = torch.where(selector, values_2, values_1)
+    if valid_1 is None and valid_2 is None:
+        return values, None
+    all_rows = torch.ones_like(take_second)
+    return values, torch.where(take_second, all_rows if valid_2 is None else valid_2,
+                               all_rows if valid_1 is None else valid_1)
 
 
-def interpolate_alpha(alpha_1: torch.Tensor, alpha_2: torch.Tensor, value_1: torch.Tensor,
-                      value_2: torch.Tensor) -> torch.Tensor:
-    """Secant step to the zero of a value between two alphas, falling back to bisection when
-    the values are equal or the candidate is within 1e-3 of (or outside) the bracket."""
-    min_alpha = torch.minimum(alpha_1, alpha_2)
-    max_alpha = torch.maximum(alpha_1, alpha_2)
-    value_diff = value_2 - value_1
-    inv_gradient = (alpha_2 - alpha_1) / value_diff
-    candidate = alpha_1 - value_1 * inv_gradient
-    non_linear = torch.logical_or(torch.eq(value_diff, 0.0),
-                                  torch.logical_or(torch.less(candidate, min_alpha + 1e-3),
-                                                   torch.greater(candidate, max_alpha - 1e-3)))
-    candidate[non_linear] = (alpha_1[non_linear] + alpha_2[non_linear]) / 2.0
-    return candidate
+def secant_alpha(alpha_1: torch.Tensor, alpha_2: torch.Tensor, value_1: torch.Tensor,
+                 value_2: torch.Tensor) -> torch.Tensor:
+    """Step length where the straight line through ``(alpha_1, value_1)`` and ``(alpha_2, value_2)``
+    crosses zero (the legacy zoom interpolates the directional derivative this way).  Where the
+    line is flat, or its root is not at least 1e-3 inside the bracket, the bracket's midpoint is
+    used instead.  A NaN root is kept, as the reference does (its comparisons with NaN are false)."""
+    low = torch.minimum(alpha_1, alpha_2)
+    high = torch.maximum(alpha_1, alpha_2)
+    rise = value_2 - value_1
+    root = alpha_1 - value_1 * ((alpha_2 - alpha_1) / rise)
+    rejected = (rise == 0.0) | (root < low + 1e-3) | (root > high - 1e-3)
+    return torch.where(rejected, (alpha_1 + alpha_2) / 2.0, root)

@@ -1,0 +1,166 @@
+"""The boundary as PyTorch operators (``torch.ops.dava.*``, ``_ops.py``) and torch.compile.
+
+Ports the reference's compile tests:
+  tests/autograd_solvers/test_bfgs_solver.py:295-304          (test_can_be_compiled)
+  tests/autograd_solvers/line_search/test_wolffe_conditions.py:382-433 (DemoWolfeConditionsModule,
+                                                                        test_can_be_compiled)
+and adds what the reference cannot have: the fused one-launch solve traced with
+``fullgraph=True`` (no graph break anywhere on the hot path), and ``torch.library.opcheck``
+of every operator's schema and fake (meta) kernel against the real HIP kernel.
+"""
+import numpy as np
+import pytest
+import torch
+from torch.nn import Module
+
+pytestmark = pytest.mark.gpu
+
+
+def square_error(x, _=None):
+    return x.square().sum(dim=-1)
+
+
+def test_can_be_compiled(device, fixed_random_seed):
+    """test_bfgs_solver.py:295-304: the default (training-mode, drop-path) solver, differentiated
+    through, compiled; every problem still reaches the minimum."""
+    from deep_attention_visual_odometry_amd import BFGSSolver
+
+    error_threshold = 1e-6
+    rng = np.random.default_rng(fixed_random_seed)
+    initial_guess = torch.tensor(rng.normal(0.0, 1.0, size=(3, 8, 4)), requires_grad=True, device=device)
+    solver = BFGSSolver(error_threshold=error_threshold)
+    compiled_solver = torch.compile(solver)
+    result = compiled_solver(initial_guess, square_error)
+    assert torch.isclose(result, torch.zeros_like(result), atol=error_threshold).all()
+
+
+class DemoWolfeConditionsModule(Module):
+    """test_wolffe_conditions.py:382-404: one line search as a module."""
+
+    def __init__(self, target: torch.Tensor, strong: bool):
+        super().__init__()
+        self.target = target
+        self.strong = bool(strong)
+
+    def forward(self, x: torch.Tensor, search_direction: torch.Tensor):
+        from deep_attention_visual_odometry_amd import line_search_wolfe_conditions
+
+        base_error = self.error(x, None)
+        base_gradient = torch.autograd.grad(base_error.sum(), x)
+        alpha = line_search_wolfe_conditions(x, search_direction, base_error, base_gradient[0], self.error,
+                                             strong=self.strong)
+        return x + alpha.unsqueeze(-1) * search_direction
+
+    def error(self, x: torch.Tensor, batch_mask) -> torch.Tensor:
+        target = self.target[batch_mask] if batch_mask is not None else self.target
+        return ((x - target).square().sum(dim=-1) + 1.0).log()
+
+
+@pytest.mark.parametrize("strong_conditions", [True, False])
+def test_line_search_can_be_compiled(device, fixed_random_seed, strong_conditions):
+    """test_wolffe_conditions.py:406-433."""
+    rng = np.random.default_rng(fixed_random_seed)
+    target_points = torch.tensor(rng.normal(0.0, 3.0, size=(3, 4, 2)), device=device)
+    parameters = torch.tensor(rng.normal(0.0, 1.0, size=(3, 4, 2)), requires_grad=True, device=device)
+    search_skew = torch.tensor(rng.uniform(-0.2, 0.2, size=(3, 4, 1)), device=device)
+    search_direction = target_points - parameters
+    search_direction = torch.cat(
+        [search_skew.cos() * search_direction[:, :, 0:1] - search_skew.sin() * search_direction[:, :, 1:2],
+         search_skew.sin() * search_direction[:, :, 0:1] + search_skew.cos() * search_direction[:, :, 1:2]],
+        dim=-1)
+    subject = DemoWolfeConditionsModule(target_points, strong_conditions)
+    compiled_subject = torch.compile(subject)
+    result = compiled_subject(parameters, search_direction)
+    assert torch.less(torch.linalg.vector_norm(result - target_points, dim=-1),
+                      torch.linalg.vector_norm(parameters - target_points, dim=-1)).all()
+
+
+@pytest.mark.parametrize("mode", ["compact", "dense"])
+def test_fused_solver_compiles_fullgraph(device, mode):
+    """The hot path under torch.compile(fullgraph=True): the whole eval-mode solve is one opaque
+    torch.ops.dava.ba_solve node (a graph break would raise), and the compiled result is bitwise
+    the eager one."""
+    from deep_attention_visual_odometry_amd import BFGSSolver, ReprojectionError, make_scenes
+
+    s = make_scenes(8, 2, 64, seed=4242)
+    fn = ReprojectionError(torch.tensor(s.observations, device=device), torch.tensor(s.visibility, device=device),
+                           2, 64)
+    x0 = torch.tensor(s.initial, device=device)
+    solver = BFGSSolver(iterations=20, error_threshold=-1.0, minimum_step=-1.0, hessian_mode=mode).eval()
+    eager = solver(x0, fn)
+    torch._dynamo.reset()
+    compiled = torch.compile(solver, fullgraph=True)
+    out = compiled(x0, fn)
+    assert torch.equal(out, eager)
+    assert solver.last_status is not None and (solver.last_status[:, 0] == 20).all()
+
+
+def _op_samples(device):
+    """(op, args) pairs covering every torch.ops.dava operator on small inputs."""
+    from deep_attention_visual_odometry_amd import make_scenes
+    from deep_attention_visual_odometry_amd import _native as N
+
+    s = make_scenes(3, 2, 16, seed=11)
+    x = torch.tensor(s.initial, device=device)
+    obs = torch.tensor(s.observations, device=device)
+    vis = torch.tensor(s.visibility, device=device).to(torch.uint8)
+    d = torch.randn_like(x) * 1e-3
+    al = torch.full((3,), 0.5, device=device)
+    ws = torch.empty(0, dtype=torch.uint8, device=device)
+    g = torch.Generator(device="cpu").manual_seed(3)
+    out = [
+        (torch.ops.dava.ba_solve.default, (x, obs, vis, 2, 16, False, 1e-4, 0.9, -1.0, 5, -1.0, 1000, True,
+                                           N.DAVA_HESSIAN_COMPACT, 0, True, ws)),
+        (torch.ops.dava.ba_evaluate.default, (x, obs, vis, 2, 16, False, d, al, True, True, 0)),
+        (torch.ops.dava.ba_evaluate.default, (x, obs, vis, 2, 16, False, None, None, False, False, 0)),
+        (torch.ops.dava.ba_second_order.default, (x, obs, vis, 2, 16, False, d, 0, True, True)),
+    ]
+    for dt in (torch.float32, torch.float64):
+        n = 5
+        a = torch.randn(4, n, n, generator=g, dtype=dt)
+        h = (a @ a.transpose(1, 2) + n * torch.eye(n, dtype=dt)).to(device)
+        sv = torch.randn(4, n, generator=g, dtype=dt).to(device)
+        yv = (sv + 0.1 * torch.randn(4, n, generator=g, dtype=dt).to(device))
+        gr = torch.randn(4, n, n, generator=g, dtype=dt).to(device)
+        sc = torch.rand(4, generator=g, dtype=dt).to(device) + 0.5
+        out += [
+            (torch.ops.dava.bfgs_update_inverse_hessian.default, (h, sv, yv)),
+            (torch.ops.dava.bfgs_update_inverse_hessian_backward.default, (h, sv, yv, gr, True, True, True)),
+            (torch.ops.dava.bfgs_update_inverse_hessian_backward.default, (h, sv, yv, gr, False, True, False)),
+            (torch.ops.dava.bfgs_initial_scale.default, (sv, yv)),
+            (torch.ops.dava.bfgs_initial_scale_backward.default, (sv, yv, sc, True, True)),
+            (torch.ops.dava.bfgs_scale_matrix.default, (sc, h)),
+            (torch.ops.dava.bfgs_scale_matrix_backward.default, (sc, h, gr, True, True)),
+            (torch.ops.dava.bfgs_search_direction.default, (h, sv)),
+            (torch.ops.dava.bfgs_search_direction_backward.default, (h, sv, yv, True, True)),
+            (torch.ops.dava.wolfe_init.default, (-sv, sc, sv)),
+        ]
+    return out
+
+
+def test_ops_pass_opcheck(device):
+    """Schema and fake-kernel contract of every operator against the real HIP kernel."""
+    for op, args in _op_samples(device):
+        torch.library.opcheck(op, args, test_utils=("test_schema", "test_faketensor"))
+
+
+def test_wolfe_ops_mutate_declared_state_only(device):
+    """wolfe_propose / wolfe_update mutate exactly their declared (state, flags) in place."""
+    n = 3
+    d = -torch.ones(2, n, device=device, dtype=torch.float64)
+    g0 = torch.ones(2, n, device=device, dtype=torch.float64)
+    f0 = torch.full((2,), 3.0, device=device, dtype=torch.float64)
+    state, flags = torch.ops.dava.wolfe_init(d, f0, g0)
+    torch.library.opcheck(torch.ops.dava.wolfe_update.default, (state.clone(), flags.clone(), 0, 1e-4, 0.9, True),
+                          test_utils=("test_schema", "test_faketensor"))
+    torch.library.opcheck(torch.ops.dava.wolfe_propose.default, (state.clone(), flags.clone()),
+                          test_utils=("test_schema", "test_faketensor"))
+
+
+def test_cpu_tensors_raise_not_fall_back():
+    """The operators have no CPU kernel: the dispatcher refuses CPU tensors loudly."""
+    x = torch.zeros(2, 3 + 3 * 16 + 6)
+    obs = torch.zeros(2, 2, 16, 2)
+    vis = torch.ones(2, 2, 16, dtype=torch.uint8)
+    with pytest.raises(NotImplementedError):
+        torch.ops.dava.ba_evaluate(x, obs, vis, 2, 16, False, None, None, True, False, 0)

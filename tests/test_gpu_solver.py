@@ -67,7 +67,31 @@ def _envelopes(x0, fn, ref, **kw):
     return env, env_i
 
 
-def _check_k100(out, ref, x0, obs, vis, m, n, distortion, env, env_intrinsics=None):
+def _report(tag, rel, env=None, extra=None):
+    """Append the per-problem parity distribution to gpurun_out/parity_distribution.jsonl (merged
+    back from the GPU box) and print it, so the judged numbers are the distribution, not pass/fail."""
+    import json
+
+    rel = rel.double()
+    rec = {"case": tag, "n": int(rel.numel()), "max_rel": float(rel.max()), "median_rel": float(rel.median()),
+           "frac_le_1e-5": float((rel <= TOL).double().mean()),
+           "n_gt_1e-5": int((rel > TOL).sum())}
+    if env is not None:
+        rec["n_outside_envelope"] = int((rel > env).sum())
+        rec["max_envelope"] = float(env.max())
+    rec.update(extra or {})
+    print("PARITY", json.dumps(rec))
+    out = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "gpurun_out")
+    try:
+        os.makedirs(out, exist_ok=True)
+        with open(os.path.join(out, "parity_distribution.jsonl"), "a") as fh:
+            fh.write(json.dumps(rec) + "\n")
+    except OSError:
+        pass
+    return rec
+
+
+def _check_k100(out, ref, x0, obs, vis, m, n, distortion, env, env_intrinsics=None, tag=None):
     """Parity after K = 100 iterations, where small two-view problems run into fp32 stagnation.
 
     Two builds of this kernel that differ only in FMA contraction (register- vs LDS-resident
@@ -85,16 +109,22 @@ def _check_k100(out, ref, x0, obs, vis, m, n, distortion, env, env_intrinsics=No
     e_ref = objective.reprojection_error(ref.double(), obs.double(), vis, m, n, distortion)
     e_0 = objective.reprojection_error(x0.double(), obs.double(), vis, m, n, distortion)
     same_objective = e_gpu <= torch.maximum(e_ref * 1.05, 1e-5 * e_0)
-    assert ((rel <= env) | same_objective).all(), (rel.tolist(), env.tolist(), e_gpu.tolist(), e_ref.tolist())
+    outside = rel > env
+    if tag is not None:
+        _report(tag, rel, env, {"n_objective_fallback": int(outside.sum())})
+    # every problem within its envelope, or (a near-tie branch at fp32 stagnation) at the same objective
+    assert (~outside | same_objective).all(), (rel.tolist(), env.tolist(), e_gpu.tolist(), e_ref.tolist())
+    # ... and the objective fallback is the exception: at most 1 problem in 8
+    assert int(outside.sum()) <= max(1, rel.numel() // 8), (rel.tolist(), env.tolist())
     if env_intrinsics is not None:
         assert ((_rel(out[:, :3], ref[:, :3]) <= env_intrinsics) | same_objective).all()
-    assert (rel <= TOL).double().mean() >= 0.5, rel
+    assert (rel <= TOL).double().mean() >= 0.75, rel
 
 
 @pytest.mark.parametrize("mode", ["dense", "compact"])
 @pytest.mark.parametrize("m,n,distortion,k,b", [
-    (2, 64, False, 5, 8), (2, 64, False, 20, 8), (2, 64, False, 100, 4),
-    (2, 128, False, 20, 4), (2, 128, False, 100, 2),
+    (2, 64, False, 5, 8), (2, 64, False, 20, 8), (2, 64, False, 100, 16),
+    (2, 128, False, 20, 4), (2, 128, False, 100, 16),
     (4, 256, False, 20, 2), (4, 256, True, 20, 2),
 ])
 def test_fixed_iterations_match_oracle(device, m, n, distortion, k, b, mode):
@@ -108,10 +138,12 @@ def test_fixed_iterations_match_oracle(device, m, n, distortion, k, b, mode):
     rel = _rel(out, ref)
     env, env_intrinsics = _envelopes(x0, fn, ref, **kw)
     if k <= 20:
+        _report(f"fixed_{mode}_M{m}_N{n}_D{int(distortion)}_K{k}_B{b}", rel, env)
         assert rel.max() <= TOL, rel
         assert (_rel(out[:, :3], ref[:, :3]) <= env_intrinsics).all()
     else:
-        _check_k100(out, ref, x0, obs, vis, m, n, distortion, env, env_intrinsics)
+        _check_k100(out, ref, x0, obs, vis, m, n, distortion, env, env_intrinsics,
+                    tag=f"fixed_{mode}_M{m}_N{n}_D{int(distortion)}_K{k}_B{b}")
     assert torch.equal(status[:, 0], rec.iterations)
     assert (status[:, 1] == 0).all()
 
@@ -131,11 +163,51 @@ def test_reference_golden_trajectories(device, case, ks, mode):
         ref = torch.tensor(g[f"{case}_k{k}"])
         rel = _rel(out, ref)
         if k <= 20:
+            _report(f"golden_{mode}_{case}_K{k}", rel)
             assert rel.max() <= TOL, (case, k, rel)
         else:
             kw = dict(iterations=k, error_threshold=-1.0, minimum_step=-1.0)
             env, _ = _envelopes(x0, fn, ref, **kw)
-            _check_k100(out, ref, x0, obs, vis, m, n, False, env)
+            _check_k100(out, ref, x0, obs, vis, m, n, False, env, tag=f"golden_{mode}_{case}_K{k}")
+
+
+_HEADLINE = {}
+
+
+def _headline_reference():
+    """The bench's own workload (bench.py defaults: seed 20251015 + 3000, C3 + Brown-Conrady,
+    K = 100 fixed): its first 16 problems, solved once by the oracle (plus the 1-ulp envelopes)."""
+    if not _HEADLINE:
+        from deep_attention_visual_odometry_amd import make_scenes
+
+        s = make_scenes(16, 4, 256, distortion=True, seed=20251015 + 3000)
+        x0, obs, vis = torch.tensor(s.initial), torch.tensor(s.observations), torch.tensor(s.visibility)
+        fn = objective.ReprojectionClosure(obs, vis, 4, 256, True)
+        kw = dict(iterations=100, error_threshold=-1.0, minimum_step=-1.0)
+        ref = solver.bfgs_solve(x0, fn, **kw)
+        env, env_i = _envelopes(x0, fn, ref, **kw)
+        _HEADLINE.update(x0=x0, obs=obs, vis=vis, ref=ref, env=env, env_i=env_i)
+    return _HEADLINE
+
+
+@pytest.mark.parametrize("mode", ["compact", "dense"])
+def test_headline_workload_matches_oracle(device, mode):
+    """Parity AT the benchmarked configuration (C3 + Brown-Conrady, P = 794, K = 100, both
+    inverse-Hessian modes), on the bench's own problems, against the oracle.  Brown-Conrady is
+    parity-unpinned against reference outputs (its module imports the absent spatial_maths): the
+    oracle restates distorted_camera_model.py:59-86.  The full distribution is reported."""
+    h = _headline_reference()
+    out, status = _gpu_solve(device, h["x0"], h["obs"], h["vis"], 4, 256, True, iterations=100,
+                             error_threshold=-1.0, minimum_step=-1.0, hessian_mode=mode)
+    rel = _rel(out, h["ref"])
+    rel_i = _rel(out[:, :3], h["ref"][:, :3])
+    rel_d = _rel(out[:, -5:], h["ref"][:, -5:])
+    _report(f"headline_{mode}_C3_BC_K100_B16", rel, h["env"],
+            {"intrinsics_max_rel": float(rel_i.max()), "distortion_max_rel": float(rel_d.max())})
+    assert (status[:, 0] == 100).all()
+    assert (rel <= h["env"]).all(), rel
+    assert (rel <= TOL).double().mean() >= 0.9, rel
+    assert (rel_i <= h["env_i"]).all(), rel_i
 
 
 def test_default_stopping_rules(device):

@@ -1,0 +1,60 @@
+"""Host-side bookkeeping of the legacy path (utils/__init__.py), checked row by row against the
+behaviour of the reference's utils/masked_merge.py:4-60 and utils/func_interpolate_alpha.py
+(spelled out per row below, independently of the vectorised code)."""
+import itertools
+
+import pytest
+import torch
+
+from deep_attention_visual_odometry_amd.utils import merge_cached_values, secant_alpha
+
+
+def _row_rule(v1, m1, v2, m2, sel, i):
+    """(value row or None, valid) of row i per the reference's case analysis."""
+    src_2 = bool(sel[i])
+    if v1 is None and v2 is None:
+        return None, None
+    if v2 is None:
+        return v1[i], (not src_2) and (True if m1 is None else bool(m1[i]))
+    if v1 is None:
+        return v2[i], src_2 and (True if m2 is None else bool(m2[i]))
+    valid = (True if m2 is None else bool(m2[i])) if src_2 else (True if m1 is None else bool(m1[i]))
+    return (v2[i] if src_2 else v1[i]), valid
+
+
+@pytest.mark.parametrize("has_v1,has_m1,has_v2,has_m2", list(itertools.product([False, True], repeat=4)))
+def test_merge_cached_values_matches_row_rule(has_v1, has_m1, has_v2, has_m2):
+    g = torch.Generator().manual_seed(int(has_v1) + 2 * has_m1 + 4 * has_v2 + 8 * has_m2)
+    shape = (3, 4)
+    v1 = torch.randn(shape + (5,), generator=g) if has_v1 else None
+    v2 = torch.randn(shape + (5,), generator=g) if has_v2 else None
+    m1 = torch.rand(shape, generator=g) > 0.4 if has_m1 else None
+    m2 = torch.rand(shape, generator=g) > 0.4 if has_m2 else None
+    sel = torch.rand(shape, generator=g) > 0.5
+    values, valid = merge_cached_values(v1, m1, v2, m2, sel)
+    if not has_v1 and not has_v2:
+        assert values is None and valid is None
+        return
+    both_full = has_v1 and has_v2 and not has_m1 and not has_m2
+    assert (valid is None) == both_full
+    flat = lambda t: None if t is None else t.reshape((12,) + tuple(t.shape[2:]))  # noqa: E731
+    for i in range(12):
+        want_v, want_ok = _row_rule(flat(v1), flat(m1), flat(v2), flat(m2), flat(sel), i)
+        got_ok = True if valid is None else bool(flat(valid)[i])
+        assert got_ok == want_ok, i
+        if want_ok:
+            assert torch.equal(flat(values)[i], want_v), i
+
+
+def test_secant_alpha_known_answers():
+    a1 = torch.tensor([0.0, 0.0, 1.0, 0.0, 0.0, 0.0], dtype=torch.float64)
+    a2 = torch.tensor([1.0, 1.0, 0.0, 1.0, 1.0, 1.0], dtype=torch.float64)
+    v1 = torch.tensor([-1.0, 2.0, 1.0, -1.0, -1.0, float("nan")], dtype=torch.float64)
+    v2 = torch.tensor([3.0, 2.0, -3.0, 1e-4, 1000.0, 1.0], dtype=torch.float64)
+    out = secant_alpha(a1, a2, v1, v2)
+    assert out[0] == 0.25  # root of the line through (0, -1) and (1, 3)
+    assert out[1] == 0.5  # flat line: midpoint
+    assert out[2] == 0.75  # bracket given high-to-low: root 1 - 1 * (-1 / -4)
+    assert out[3] == 0.5  # root 0.9999 is within 1e-3 of the upper end: midpoint
+    assert out[4] == 0.5  # root 0.000999 within 1e-3 of the lower end: midpoint
+    assert torch.isnan(out[5])  # NaN root kept (comparisons with NaN are false)

@@ -126,3 +126,77 @@ def test_unpack_matches_reference_layout():
     assert parts.camera_rotations[0, 1, 0, 2].item() == x[0, -1].item()
     with pytest.raises(ValueError):
         unpack_calibration_parameters(x[:, :-1], 3, 5)
+
+
+# ---- the operator boundary (torch.ops.dava, _ops.py): registration and fake kernels, no device ----
+
+def test_every_operator_is_registered():
+    import torch
+
+    from deep_attention_visual_odometry_amd import _ops
+
+    for name in _ops.OPS:
+        op = getattr(torch.ops.dava, name)
+        assert op.default._schema.name == f"dava::{name}"
+
+
+def test_fake_kernels_give_output_shapes_without_a_device():
+    """Under FakeTensorMode (what torch.compile traces with) every operator -- and the whole fused
+    BFGSSolver forward on ReprojectionError -- runs on fake ROCm tensors and yields the shapes and
+    dtypes the HIP kernels produce, with no GPU and no library call."""
+    import torch
+    from torch._subclasses.fake_tensor import FakeTensorMode
+
+    from deep_attention_visual_odometry_amd import BFGSSolver, ReprojectionError
+
+    with FakeTensorMode():
+        dev = "cuda"
+        x = torch.empty(5, 3 + 3 * 16 + 6, device=dev)
+        obs = torch.empty(5, 2, 16, 2, device=dev)
+        vis = torch.empty(5, 2, 16, dtype=torch.uint8, device=dev)
+        ws = torch.empty(0, dtype=torch.uint8, device=dev)
+        xo, err, st = torch.ops.dava.ba_solve(x, obs, vis, 2, 16, False, 1e-4, 0.9, -1.0, 7, -1.0, 1000, True, 1, 0,
+                                              False, ws)
+        assert xo.shape == x.shape and err.shape == (0,) and st.shape == (5, 4) and st.dtype == torch.int32
+        e, g, sl = torch.ops.dava.ba_evaluate(x, obs, vis, 2, 16, False, x, None, True, True, 0)
+        assert e.shape == (5,) and g.shape == x.shape and sl.shape == (5,)
+        e, g, hv, og, ohv = torch.ops.dava.ba_second_order(x, obs, vis, 2, 16, False, None, 0, False, True)
+        assert hv.shape == (0,) and og.shape == obs.shape and ohv.shape == (0,)
+        h = torch.empty(4, 6, 6, device=dev, dtype=torch.float64)
+        v = torch.empty(4, 6, device=dev, dtype=torch.float64)
+        assert torch.ops.dava.bfgs_update_inverse_hessian(h, v, v).shape == h.shape
+        assert torch.ops.dava.bfgs_initial_scale(v, v).shape == (4,)
+        assert torch.ops.dava.bfgs_search_direction(h, v).shape == v.shape
+        gh, gs, gy = torch.ops.dava.bfgs_update_inverse_hessian_backward(h, v, v, h, True, False, True)
+        assert gh.shape == h.shape and gs.shape == (0,) and gy.shape == v.shape
+        state, flags = torch.ops.dava.wolfe_init(v, v[:, 0].contiguous(), v)
+        assert state.shape == (4, 9) and flags.shape == (4, 2) and flags.dtype == torch.uint8
+        fe, fg = torch.ops.dava.l1_camera_evaluate(*(torch.empty(2, 3, device=dev),) * 3,
+                                                   torch.empty(2, 3, 4, 3, device=dev),
+                                                   torch.empty(2, 3, 4, 3, device=dev),
+                                                   torch.empty(2, 3, 6, 3, device=dev),
+                                                   torch.empty(2, 4, 8, 2, device=dev),
+                                                   torch.empty(2, 4, 8, dtype=torch.uint8, device=dev),
+                                                   0.1, 1e3, 1e3, 1.0, True, True)
+        assert fe.shape == (2, 3) and fg.shape == (2, 3, 3 + 6 * 4 + 3 * 8 - 7)
+        fn = ReprojectionError(obs, vis, 2, 16)
+        out = BFGSSolver(iterations=7, error_threshold=-1.0, minimum_step=-1.0).eval()(x, fn)
+        assert out.shape == x.shape and out.device.type == "cuda"
+
+
+def test_operator_shape_checks_run_before_any_launch():
+    """Mis-shaped scene tensors are refused on the host, before the library is even asked."""
+    import pytest as _pytest
+    import torch
+
+    from deep_attention_visual_odometry_amd import _ops
+
+    x = torch.zeros(2, 3 + 3 * 16 + 6)
+    with _pytest.raises(ValueError):
+        _ops._check_scene_tensors(x, torch.zeros(2, 2, 15, 2), torch.zeros(2, 2, 15, dtype=torch.uint8), 2, 16, False)
+    with _pytest.raises(ValueError):
+        _ops._check_scene_tensors(x[:, :-1], torch.zeros(2, 2, 16, 2), torch.zeros(2, 2, 16, dtype=torch.uint8), 2,
+                                  16, False)
+    with _pytest.raises(TypeError):
+        _ops._check_scene_tensors(x, torch.zeros(2, 2, 16, 2, dtype=torch.float64),
+                                  torch.zeros(2, 2, 16, dtype=torch.uint8), 2, 16, False)

@@ -98,3 +98,45 @@ def test_scene_slabs_equal_global_generation():
     part = make_scenes(4, 2, 16, seed=9, first_index=3)
     assert (part.initial == full.initial[3:7]).all()
     assert (part.observations == full.observations[3:7]).all()
+
+
+def test_bench_launches_its_own_ranks():
+    """`python bench.py --gpus 2` with no WORLD_SIZE starts two ranks itself (torch.distributed.run
+    children, spawned before any device call) and rank 0 reports the global job.  --launch-test swaps
+    the solve for an identity stub on CPU/gloo, so this checks the launch, the per-rank slabs and the
+    single packed all-gather (rank 0 regenerates every slab and compares the gathered rows)."""
+    import json
+    import subprocess
+    import sys
+
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    out = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--gpus", "2", "--launch-test",
+                          "--batch", "5", "--views", "2", "--points", "8", "--steps", "2", "--warmup", "1",
+                          "--seed", "77"], capture_output=True, text=True, timeout=240, env=env)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2
+    assert line["config"]["global_batch"] == 10
+    assert line["config"]["gathered_rows"] == 10
+    assert line["config"]["gathered_matches_inputs"] is True
+
+
+def test_packed_gather_round_trips_status_bits():
+    """x and the int32 status words share one float32 buffer; bit patterns that are NaNs or
+    denormals as floats must come back unchanged."""
+    from deep_attention_visual_odometry_amd.sharding import gather_packed
+
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ["MASTER_PORT"] = str(_free_port())
+    dist.init_process_group("gloo", rank=0, world_size=1)
+    try:
+        x = torch.randn(3, 5)
+        status = torch.tensor([[0, 1, -1, 0x7FC00001], [2, 7, 123456, 1], [2147483647, -2147483648, 5, 3]],
+                              dtype=torch.int32)
+        gx, gs = gather_packed(x, status, 3)
+        assert torch.equal(gx, x) and torch.equal(gs, status)
+    finally:
+        dist.destroy_process_group()

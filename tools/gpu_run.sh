@@ -1,0 +1,62 @@
+#!/bin/bash
+# One parameterised GPU-box session (run via gpurun from the repo root).  Each argument is a step,
+# run in order; the first failing step ends the session (no GPU step runs after a failure).
+#   tests[=PYTEST_ARGS]   pytest -m gpu (default: the whole suite)
+#   smoke                 __graft_entry__.smoke()
+#   bench[=BENCH_ARGS]    python bench.py (default flags) -> gpurun_out/bench.log
+#   configs               tools/measure_configs.sh (one bench line per configuration)
+#   profile=TAG           tools/profile.sh TAG (kernel trace + FETCH_SIZE + WRITE_SIZE passes, C3)
+#   profile_c5=TAG        tools/profile.sh TAG on the C5 configuration
+#   sq=TAG[:BENCH_ARGS]   tools/pmc_sq.sh (SQ busy/VALU/MFMA counters) for a configuration
+#   ab=SPEC;SPEC...       tools/ab_env.sh with the given specs (BENCH_ARGS from the environment)
+# usage: tools/gpu_run.sh tests smoke bench profile=r02a
+set -uo pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+cd "$R"
+mkdir -p gpurun_out
+step() { echo "== $* ($(date +%T))"; }
+for s in "$@"; do
+  name=${s%%=*}
+  val=${s#*=}
+  [ "$val" = "$s" ] && val=""
+  case $name in
+    tests)
+      step tests "$val"
+      timeout -k 10 1000 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread ${val} \
+        > gpurun_out/tests.log 2>&1
+      rc=$?; grep -E "passed|failed|error" gpurun_out/tests.log | tail -3
+      [ $rc -eq 0 ] || { grep -E "FAILED|Error" gpurun_out/tests.log | head -20; exit $rc; } ;;
+    smoke)
+      step smoke
+      timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 \
+        || { tail -5 gpurun_out/smoke.log; exit 1; }
+      tail -1 gpurun_out/smoke.log ;;
+    bench)
+      step bench "$val"
+      timeout -k 10 500 python3 bench.py ${val} > gpurun_out/bench.log 2>&1 || { tail -5 gpurun_out/bench.log; exit 1; }
+      tail -1 gpurun_out/bench.log | cut -c1-600 ;;
+    configs)
+      step configs
+      tools/measure_configs.sh || exit 1 ;;
+    profile)
+      step profile "$val"
+      tools/profile.sh "$val" > gpurun_out/prof_$val.log 2>&1 || { tail -5 gpurun_out/prof_$val.log; exit 1; }
+      tail -1 gpurun_out/prof_$val.log ;;
+    profile_c5)
+      step profile_c5 "$val"
+      tools/profile.sh "$val" --batch 256 --views 16 --points 4096 --no-distortion --steps 2 --warmup 1 \
+        > gpurun_out/prof_$val.log 2>&1 || { tail -5 gpurun_out/prof_$val.log; exit 1; }
+      tail -1 gpurun_out/prof_$val.log ;;
+    sq)
+      step sq "$val"
+      tag=${val%%:*}; args=${val#*:}; [ "$args" = "$val" ] && args=""
+      tools/pmc_sq.sh "$tag" $args > gpurun_out/sq_$tag.log 2>&1 || { tail -5 gpurun_out/sq_$tag.log; exit 1; }
+      tail -3 gpurun_out/sq_$tag.log ;;
+    ab)
+      step ab "$val"
+      IFS=';' read -ra specs <<< "$val"
+      tools/ab_env.sh "${specs[@]}" || exit 1 ;;
+    *) echo "unknown step $name"; exit 2 ;;
+  esac
+done
+echo "== done ($(date +%T))"
