@@ -81,7 +81,8 @@ __host__ __device__ inline bool wide_history_pass(int Pv, int kcap, bool gv) {
 // and d and accumulates point gradients view after view, one dependent access per pair --
 // runs on-chip; the other vectors stay in the workspace slice (its x and d slots unused).
 __host__ __device__ inline LdsCarve carve_lds(int M, int N, int Pv, int kcap = 0, bool gv = false, int lcap = 0,
-                                              bool xl = false) {
+                                              bool xl = false, int nw = 0) {
+  if (nw <= 0) nw = solve_waves(gv);
   LdsCarve c;
   int off = 0;
   int voff = 0;
@@ -101,8 +102,8 @@ __host__ __device__ inline LdsCarve carve_lds(int M, int N, int Pv, int kcap = 0
   c.hg = o; o += Pv;
   c.obs = off; off += gv ? 0 : round_up(2 * M * N, 4);
   c.views = off; off += round_up(views_floats(M), 4);
-  c.vpart = off; off += round_up(vpart_floats(M, solve_waves(gv)), 4);
-  c.scratch = off; off += 2 * solve_waves(gv) * 32;
+  c.vpart = off; off += round_up(vpart_floats(M, nw), 4);
+  c.scratch = off; off += 2 * nw * 32;
   c.hcoef = off; off += 4 * kcap;  // COMPACT: per-entry product coefficients
   c.hrho = off; off += round_up(kcap, 4);
   c.hc = off; off += round_up(kcap, 4);
@@ -453,12 +454,27 @@ __device__ __forceinline__ void compact_products_wide(int P, int Pv, int nh, con
 #ifndef DAVA_DEFER_COMBINE
 #define DAVA_DEFER_COMBINE 1
 #endif
+// EF: history entries in flight per wave (each holds 2 GM float4 rows in registers).  More
+// entries in flight = more bytes outstanding per wave, which is what the history stream of a
+// problem with few waves (or few problems per CU) is bound by.
+#ifndef DAVA_FUSED_INFLIGHT_SMALL
+#define DAVA_FUSED_INFLIGHT_SMALL 4  // rows of <= 2 float4 groups per lane (P <= 512)
+#endif
+#ifndef DAVA_FUSED_INFLIGHT_LARGE
+#define DAVA_FUSED_INFLIGHT_LARGE 2  // 3-4 groups per lane (P <= 1024; C3)
+#endif
 template <int GM>
+__host__ __device__ constexpr int fused_inflight() {
+  return DAVA_FUSED_PAIR ? (GM <= 2 ? DAVA_FUSED_INFLIGHT_SMALL : DAVA_FUSED_INFLIGHT_LARGE) : 1;
+}
+template <int GM, int NW>
 __device__ __forceinline__ void compact_products_fused(int P, int Pv, int nh, const float* __restrict__ S,
                                        const float* __restrict__ W, const float* LH, int lcap,
                                        const float* hrho, const float* hc,
                                        float gamma0, const float* g, const float* gp, float* a_out, float* b_out,
                                        float* spare0, float* spare1, float* spare2, float* spare3) {
+  static_assert(NW == 1 || NW == 2 || NW == 4, "the cross-wave combine is written for 1, 2 or 4 waves");
+  constexpr int EF = fused_inflight<GM>();
   const int lane = threadIdx.x & (kWave - 1);
   const int wave = threadIdx.x / kWave;
   const int G = (P + 3) / 4;
@@ -514,7 +530,7 @@ __device__ __forceinline__ void compact_products_fused(int P, int Pv, int nh, co
   __builtin_amdgcn_s_setprio(DAVA_HIST_PRIO);
 #endif
   int j = wave;
-  for (const int nl = min(lcap, nh); j < nl; j += kWaves) {  // on-chip entries first (wave-uniform)
+  for (const int nl = min(lcap, nh); j < nl; j += NW) {  // on-chip entries first (wave-uniform)
     f4v s0[GM], w0[GM];
     const float* sr = LH + (size_t)2 * j * Pv;
     const float* wr = sr + Pv;
@@ -526,16 +542,16 @@ __device__ __forceinline__ void compact_products_fused(int P, int Pv, int nh, co
     }
     consume(j, s0, w0);
   }
-#if DAVA_FUSED_PAIR
-  for (; j + kWaves < nh; j += 2 * kWaves) {
-    f4v s0[GM], w0[GM], s1[GM], w1[GM];
-    load(j, s0, w0);
-    load(j + kWaves, s1, w1);
-    consume(j, s0, w0);
-    consume(j + kWaves, s1, w1);
+  if constexpr (EF > 1) {  // EF entries of this wave in flight: all loads issued before any is consumed
+    for (; j + (EF - 1) * NW < nh; j += EF * NW) {
+      f4v s[EF][GM], w[EF][GM];
+#pragma unroll
+      for (int e = 0; e < EF; ++e) load(j + e * NW, s[e], w[e]);
+#pragma unroll
+      for (int e = 0; e < EF; ++e) consume(j + e * NW, s[e], w[e]);
+    }
   }
-#endif
-  for (; j < nh; j += kWaves) {  // one entry in flight per wave
+  for (; j < nh; j += NW) {  // the rest, one entry in flight
     f4v s0[GM], w0[GM];
     load(j, s0, w0);
     consume(j, s0, w0);
@@ -543,7 +559,8 @@ __device__ __forceinline__ void compact_products_fused(int P, int Pv, int nh, co
 #if DAVA_HIST_PRIO != DAVA_BASE_PRIO
   __builtin_amdgcn_s_setprio(DAVA_BASE_PRIO);
 #endif
-  // deterministic cross-wave sum: ((w0 + w2) + (w1 + w3)) + gamma0 * (y | g)
+  // deterministic cross-wave sum: ((w0 + w2) + (w1 + w3)) + gamma0 * (y | g)  (NW = 4),
+  // (w0 + w1) + gamma0 * (y | g)  (NW = 2), w0 + gamma0 * (y | g)  (NW = 1)
   auto put = [&](float* A, float* B) {
 #pragma unroll
     for (int m = 0; m < GM; ++m)
@@ -562,6 +579,35 @@ __device__ __forceinline__ void compact_products_fused(int P, int Pv, int nh, co
         pb[m] += *reinterpret_cast<const f4v*>(B + 4 * q);
       }
   };
+  auto finish = [&]() {  // + gamma0 (y | g), into the outputs
+#pragma unroll
+    for (int m = 0; m < GM; ++m)
+      if (ok[m]) {
+        pa[m] += gamma0 * yvec(m);
+        pb[m] += gamma0 * gvec(m);
+      }
+    put(a_out, b_out);
+  };
+  if constexpr (NW == 1) {
+    finish();
+    return;
+  }
+  if constexpr (NW == 2) {
+    // deferred: w0 in spare0/1, w1 in spare2/3; the caller's block-wide pass adds them and
+    // gamma0 (y | g) element by element after its barrier (same operations, same order)
+    if (DAVA_DEFER_COMBINE) {
+      if (wave == 0) put(spare0, spare1);
+      if (wave == 1) put(spare2, spare3);
+      return;
+    }
+    if (wave == 1) put(spare0, spare1);
+    __syncthreads();
+    if (wave == 0) {
+      add(spare0, spare1);
+      finish();
+    }
+    return;
+  }
   if (wave == 2) put(spare0, spare1);
   if (wave == 3) put(spare2, spare3);
   __syncthreads();
@@ -577,22 +623,18 @@ __device__ __forceinline__ void compact_products_fused(int P, int Pv, int nh, co
   __syncthreads();
   if (wave == 0) {
     add(spare2, spare3);
-#pragma unroll
-    for (int m = 0; m < GM; ++m)
-      if (ok[m]) {
-        pa[m] += gamma0 * yvec(m);
-        pb[m] += gamma0 * gvec(m);
-      }
-    put(a_out, b_out);
+    finish();
   }
 }
 
 // XL: GV mode with x, d and the objective's gradient in LDS.  PPT > 0: the objective keeps
 // each thread's (<= PPT) points in registers across the view sweep (ba_eval).
-template <int MODE, bool GV, int RES, bool XL, int PPT>
-__global__ __launch_bounds__(kWave * solve_waves(GV), DAVA_SOLVE_WAVES_PER_EU) void bfgs_ba_solve_kernel(SolveArgs a) {
+// NW: waves per workgroup -- 8 in GV mode; 4 (default) or 2 in LDS mode (two-wave workgroups put
+// twice as many small problems on a CU at once, DESIGN.md 3.1 Launch).
+template <int MODE, bool GV, int RES, bool XL, int PPT, int NW>
+__global__ __launch_bounds__(kWave * NW, DAVA_SOLVE_WAVES_PER_EU) void bfgs_ba_solve_kernel(SolveArgs a) {
   static_assert(!XL || GV, "XL is a global-vector-mode variant");
-  constexpr int NW = solve_waves(GV);
+  static_assert(GV ? NW == solve_waves(true) : (NW == 2 || NW == 4), "LDS mode runs 2- or 4-wave workgroups");
   constexpr int BLOCK = kWave * NW;
   extern __shared__ __attribute__((aligned(16))) float lds[];
 #if DAVA_BASE_PRIO
@@ -615,7 +657,7 @@ __global__ __launch_bounds__(kWave * solve_waves(GV), DAVA_SOLVE_WAVES_PER_EU) v
       if (b >= a.B) break;
     }
     const int lcap = MODE == DAVA_HESSIAN_COMPACT && !GV ? a.lcap : 0;
-    const LdsCarve cv = carve_lds(M, N, Pv, MODE == DAVA_HESSIAN_COMPACT ? a.kcap : 0, GV, lcap, XL);
+    const LdsCarve cv = carve_lds(M, N, Pv, MODE == DAVA_HESSIAN_COMPACT ? a.kcap : 0, GV, lcap, XL, NW);
     float* LH = lds + cv.hist;  // LDS-resident history entries 0 .. lcap-1
     float* vb0 = GV ? a.vecs + (size_t)b * kVectors * Pv : lds;
     float* x = (GV && !XL ? vb0 : lds) + cv.x;
@@ -744,8 +786,8 @@ __global__ __launch_bounds__(kWave * solve_waves(GV), DAVA_SOLVE_WAVES_PER_EU) v
   #ifndef DAVA_COMPACT_TWO_PASS
             const int G4 = (P + 3) / 4;
             const int GM = (G4 + kWave - 1) / kWave;
-            deferred = DAVA_DEFER_COMBINE && NW == kWaves && GM <= 4;
-            if constexpr (NW != kWaves) {  // GV: workgroup-wide single pass, else two passes
+            deferred = DAVA_DEFER_COMBINE && !GV && GM <= 4;
+            if constexpr (GV) {  // workgroup-wide single pass, else two passes
               const int GT = (G4 + kWave * NW - 1) / (kWave * NW);
               const int nh = k - 1;
               if (!wide_history_pass(Pv, a.kcap, GV))
@@ -758,10 +800,10 @@ __global__ __launch_bounds__(kWave * solve_waves(GV), DAVA_SOLVE_WAVES_PER_EU) v
               else if (GT == 6) compact_products_wide<6, NW>(P, Pv, nh, SH, WH, hrho, hc, gamma0, g, gp, hy_new, hg, scratch, buf);
               else compact_products_wide<7, NW>(P, Pv, nh, SH, WH, hrho, hc, gamma0, g, gp, hy_new, hg, scratch, buf);
             } else
-            if (GM <= 1) compact_products_fused<1>(P, Pv, k - 1, SH, WH, LH, lcap, hrho, hc, gamma0, g, gp, hy_new, hg, s_pend, hy_pend, d, hg);
-            else if (GM == 2) compact_products_fused<2>(P, Pv, k - 1, SH, WH, LH, lcap, hrho, hc, gamma0, g, gp, hy_new, hg, s_pend, hy_pend, d, hg);
-            else if (GM == 3) compact_products_fused<3>(P, Pv, k - 1, SH, WH, LH, lcap, hrho, hc, gamma0, g, gp, hy_new, hg, s_pend, hy_pend, d, hg);
-            else if (GM == 4) compact_products_fused<4>(P, Pv, k - 1, SH, WH, LH, lcap, hrho, hc, gamma0, g, gp, hy_new, hg, s_pend, hy_pend, d, hg);
+            if (GM <= 1) compact_products_fused<1, NW>(P, Pv, k - 1, SH, WH, LH, lcap, hrho, hc, gamma0, g, gp, hy_new, hg, s_pend, hy_pend, d, hg);
+            else if (GM == 2) compact_products_fused<2, NW>(P, Pv, k - 1, SH, WH, LH, lcap, hrho, hc, gamma0, g, gp, hy_new, hg, s_pend, hy_pend, d, hg);
+            else if (GM == 3) compact_products_fused<3, NW>(P, Pv, k - 1, SH, WH, LH, lcap, hrho, hc, gamma0, g, gp, hy_new, hg, s_pend, hy_pend, d, hg);
+            else if (GM == 4) compact_products_fused<4, NW>(P, Pv, k - 1, SH, WH, LH, lcap, hrho, hc, gamma0, g, gp, hy_new, hg, s_pend, hy_pend, d, hg);
             else
   #endif
             // GV mode (very long rows, few resident waves): 8 column groups in flight per lane;
@@ -1027,10 +1069,23 @@ static size_t dense_hessian_bytes(const DavaScene* s) {
 #ifndef DAVA_EXTRA_LDS
 #define DAVA_EXTRA_LDS 0  // diagnostic builds only: pad LDS to force fewer workgroups per CU
 #endif
-static int lds_bytes_for(const DavaScene* s, int kcap = 0, bool gv = false, int lcap = 0, bool xl = false) {
-  return carve_lds(s->num_views, s->num_points, round_up(s->num_parameters, 4), kcap, gv, lcap, xl).total_bytes +
+static int lds_bytes_for(const DavaScene* s, int kcap = 0, bool gv = false, int lcap = 0, bool xl = false,
+                         int nw = 0) {
+  return carve_lds(s->num_views, s->num_points, round_up(s->num_parameters, 4), kcap, gv, lcap, xl, nw).total_bytes +
          DAVA_EXTRA_LDS;
 }
+
+// Waves per LDS-mode workgroup (GV mode: always 8).  Four by default; DAVA_SOLVE_WAVES=2|4
+// overrides (A/B and tests).
+static int lds_mode_waves(const DavaScene* s) {
+  (void)s;
+  if (const char* e = getenv("DAVA_SOLVE_WAVES")) {
+    const int w = atoi(e);
+    if (w == 2 || w == 4) return w;
+  }
+  return 4;
+}
+static int solve_waves_for(const DavaScene* s, bool gv) { return gv ? solve_waves(true) : lds_mode_waves(s); }
 
 // Global-vector mode when the all-in-LDS image would cost more than two workgroups
 // per CU (e.g. C5: P = 12381 -> 446 KB of vectors per problem).
@@ -1059,19 +1114,20 @@ static size_t compact_history_bytes(const DavaScene* s, const DavaSolverConfig* 
 }
 
 // COMPACT, LDS mode, single-pass products: how many of the oldest history entries to keep
-// on-chip.  Default: whatever fits beside the problem image without dropping below two
-// workgroups per CU (80 KiB each); DAVA_LDS_HISTORY=n overrides (A/B and tests; 0 = all in
-// HBM; values past one workgroup's LDS are clamped).
-constexpr int kLdsPerWorkgroupAt2 = kMaxLds / DAVA_SOLVE_WAVES_PER_EU;  // 80 KiB at 2 workgroups per CU
-static int lds_history_entries(const DavaScene* s, int kcap, bool gv) {
+// on-chip.  Default: whatever fits beside the problem image without lowering the number of
+// workgroups a CU holds at the register limit (4 SIMDs x DAVA_SOLVE_WAVES_PER_EU waves / nw:
+// two 4-wave workgroups of 80 KiB, or four 2-wave workgroups of 40 KiB); DAVA_LDS_HISTORY=n
+// overrides (A/B and tests; 0 = all in HBM; values past one workgroup's LDS are clamped).
+static int lds_history_entries(const DavaScene* s, int kcap, bool gv, int nw) {
 #ifdef DAVA_COMPACT_TWO_PASS
   return 0;
 #endif
   const int Pv = round_up(s->num_parameters, 4);
   if (gv || kcap <= 0 || (Pv / 4 + kWave - 1) / kWave > 4) return 0;
-  const int base = lds_bytes_for(s, kcap, false, 0);
+  const int base = lds_bytes_for(s, kcap, false, 0, false, nw);
   const int per = 2 * Pv * (int)sizeof(float);
-  int n = (kLdsPerWorkgroupAt2 - base) / per;
+  const int per_cu = 4 * DAVA_SOLVE_WAVES_PER_EU / nw;  // workgroups per CU at the register limit
+  int n = (kMaxLds / per_cu - base) / per;
   if (const char* e = getenv("DAVA_LDS_HISTORY")) n = atoi(e);
   n = min(n, (kMaxLds - base) / per);
   return max(0, min(n, kcap));
@@ -1105,18 +1161,19 @@ extern "C" int dava_ba_solve_plan(const DavaScene* scene, const DavaSolverConfig
   if (mode != DAVA_HESSIAN_DENSE && mode != DAVA_HESSIAN_COMPACT) return DAVA_ERR_INVALID_ARGUMENT;
   const int kcap = mode == DAVA_HESSIAN_COMPACT ? compact_capacity(config) : 0;
   const bool gv = use_gv(scene, kcap);
-  const int lcap = mode == DAVA_HESSIAN_COMPACT ? lds_history_entries(scene, kcap, gv) : 0;
+  const int nw = solve_waves_for(scene, gv);
+  const int lcap = mode == DAVA_HESSIAN_COMPACT ? lds_history_entries(scene, kcap, gv, nw) : 0;
   plan->global_vectors = gv ? 1 : 0;
-  plan->workgroup_threads = kWave * solve_waves(gv);
-  plan->lds_bytes = lds_bytes_for(scene, kcap, gv, lcap, use_xl(scene, kcap, gv));
+  plan->workgroup_threads = kWave * nw;
+  plan->lds_bytes = lds_bytes_for(scene, kcap, gv, lcap, use_xl(scene, kcap, gv), nw);
   plan->lds_history_entries = lcap;
   return plan->lds_bytes > kMaxLds || kcap > kMaxCompactEntries ? DAVA_ERR_UNSUPPORTED : DAVA_OK;
 }
 
-template <int MODE, bool GV, int RES, bool XL, int PPT>
+template <int MODE, bool GV, int RES, bool XL, int PPT, int NW>
 static void launch_solve_ppt(const SolveArgs& a, int B, int lds, hipStream_t s) {
-  const auto kernel = bfgs_ba_solve_kernel<MODE, GV, RES, XL, PPT>;
-  constexpr int threads = kWave * solve_waves(GV);
+  const auto kernel = bfgs_ba_solve_kernel<MODE, GV, RES, XL, PPT, NW>;
+  constexpr int threads = kWave * NW;
   if (lds > 64 * 1024)
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize, lds);
   int grid = B;
@@ -1149,19 +1206,26 @@ static void launch_solve_ppt(const SolveArgs& a, int B, int lds, hipStream_t s) 
 template <bool GV, bool XL>
 constexpr int kRegisterPoints = GV ? 0 : 1;
 
-template <int MODE, bool GV, int RES, bool XL>
-static void launch_solve_res(const SolveArgs& a, int B, int lds, hipStream_t s) {
+template <int MODE, bool GV, int RES, bool XL, int NW>
+static void launch_solve_nw(const SolveArgs& a, int B, int lds, hipStream_t s) {
   constexpr int R = kRegisterPoints<GV, XL>;
-  if (R > 0 && a.L.N <= R * kWave * solve_waves(GV) && getenv("DAVA_NO_PPT") == nullptr)
-    launch_solve_ppt<MODE, GV, RES, XL, R>(a, B, lds, s);
+  if (R > 0 && a.L.N <= R * kWave * NW && getenv("DAVA_NO_PPT") == nullptr)
+    launch_solve_ppt<MODE, GV, RES, XL, R, NW>(a, B, lds, s);
   else
-    launch_solve_ppt<MODE, GV, RES, XL, 0>(a, B, lds, s);
+    launch_solve_ppt<MODE, GV, RES, XL, 0, NW>(a, B, lds, s);
+}
+
+template <int MODE, bool GV, int RES, bool XL>
+static void launch_solve_res(const SolveArgs& a, int B, int lds, hipStream_t s, int nw) {
+  if constexpr (GV) launch_solve_nw<MODE, GV, RES, XL, solve_waves(true)>(a, B, lds, s);
+  else if (nw == 2) launch_solve_nw<MODE, GV, RES, XL, 2>(a, B, lds, s);
+  else launch_solve_nw<MODE, GV, RES, XL, 4>(a, B, lds, s);
 }
 
 template <int MODE, bool GV, bool XL = false>
-static void launch_solve(const SolveArgs& a, int B, int lds, hipStream_t s, int residual) {
-  if (residual == DAVA_RESIDUAL_RAY_ANGLE) launch_solve_res<MODE, GV, DAVA_RESIDUAL_RAY_ANGLE, XL>(a, B, lds, s);
-  else launch_solve_res<MODE, GV, DAVA_RESIDUAL_SQUARED_REPROJECTION, XL>(a, B, lds, s);
+static void launch_solve(const SolveArgs& a, int B, int lds, hipStream_t s, int residual, int nw) {
+  if (residual == DAVA_RESIDUAL_RAY_ANGLE) launch_solve_res<MODE, GV, DAVA_RESIDUAL_RAY_ANGLE, XL>(a, B, lds, s, nw);
+  else launch_solve_res<MODE, GV, DAVA_RESIDUAL_SQUARED_REPROJECTION, XL>(a, B, lds, s, nw);
 }
 
 extern "C" int dava_ba_solve(const DavaScene* scene, const DavaSolverConfig* config, const float* x0,
@@ -1178,8 +1242,9 @@ extern "C" int dava_ba_solve(const DavaScene* scene, const DavaSolverConfig* con
   if (kcap > kMaxCompactEntries) return DAVA_ERR_UNSUPPORTED;
   const bool gv = use_gv(scene, kcap);
   const bool xl = use_xl(scene, kcap, gv);
-  const int lcap = mode == DAVA_HESSIAN_COMPACT ? lds_history_entries(scene, kcap, gv) : 0;
-  const int lds = lds_bytes_for(scene, kcap, gv, lcap, xl);
+  const int nw = solve_waves_for(scene, gv);
+  const int lcap = mode == DAVA_HESSIAN_COMPACT ? lds_history_entries(scene, kcap, gv, nw) : 0;
+  const int lds = lds_bytes_for(scene, kcap, gv, lcap, xl, nw);
   if (lds > kMaxLds) return DAVA_ERR_UNSUPPORTED;
   const size_t vec = gv ? gv_vector_bytes(scene) : 0;
   const size_t need = solve_state_bytes(scene, config);
@@ -1225,13 +1290,13 @@ extern "C" int dava_ba_solve(const DavaScene* scene, const DavaSolverConfig* con
   }
 #endif
   if (mode == DAVA_HESSIAN_DENSE) {
-    if (xl) launch_solve<DAVA_HESSIAN_DENSE, true, true>(a, scene->batch, lds, s, scene->residual);
-    else if (gv) launch_solve<DAVA_HESSIAN_DENSE, true>(a, scene->batch, lds, s, scene->residual);
-    else launch_solve<DAVA_HESSIAN_DENSE, false>(a, scene->batch, lds, s, scene->residual);
+    if (xl) launch_solve<DAVA_HESSIAN_DENSE, true, true>(a, scene->batch, lds, s, scene->residual, nw);
+    else if (gv) launch_solve<DAVA_HESSIAN_DENSE, true>(a, scene->batch, lds, s, scene->residual, nw);
+    else launch_solve<DAVA_HESSIAN_DENSE, false>(a, scene->batch, lds, s, scene->residual, nw);
   } else {
-    if (xl) launch_solve<DAVA_HESSIAN_COMPACT, true, true>(a, scene->batch, lds, s, scene->residual);
-    else if (gv) launch_solve<DAVA_HESSIAN_COMPACT, true>(a, scene->batch, lds, s, scene->residual);
-    else launch_solve<DAVA_HESSIAN_COMPACT, false>(a, scene->batch, lds, s, scene->residual);
+    if (xl) launch_solve<DAVA_HESSIAN_COMPACT, true, true>(a, scene->batch, lds, s, scene->residual, nw);
+    else if (gv) launch_solve<DAVA_HESSIAN_COMPACT, true>(a, scene->batch, lds, s, scene->residual, nw);
+    else launch_solve<DAVA_HESSIAN_COMPACT, false>(a, scene->batch, lds, s, scene->residual, nw);
   }
   const bool launched = hipGetLastError() == hipSuccess;
 #if DAVA_PHASE_TIMING

@@ -21,17 +21,25 @@ def square_error(x, _=None):
 
 
 def test_can_be_compiled(device, fixed_random_seed):
-    """test_bfgs_solver.py:295-304: the default (training-mode, drop-path) solver, differentiated
-    through, compiled; every problem still reaches the minimum."""
+    """test_bfgs_solver.py:295-304: the training-mode solver (create_graph, since the guess
+    requires grad), compiled; every problem reaches the minimum.  (Calling backward on the compiled
+    result is a double backward, which torch.compile's aot_autograd does not support; the eager
+    gradient through the solve is covered in test_gpu_solve_grad.py.)
+
+    drop_path_p = 0: with the reference's default 0.1 each of the 96 problems is dropped for good
+    with probability 0.1 per iteration (bfgs_solver.py:121-125), so the reference's own assertion
+    fails for a few problems on almost every draw; drop-path itself is covered
+    with a deterministic RNG in test_gpu_generic.py::test_training_mode_matches_reference."""
     from deep_attention_visual_odometry_amd import BFGSSolver
 
     error_threshold = 1e-6
     rng = np.random.default_rng(fixed_random_seed)
     initial_guess = torch.tensor(rng.normal(0.0, 1.0, size=(3, 8, 4)), requires_grad=True, device=device)
-    solver = BFGSSolver(error_threshold=error_threshold)
+    solver = BFGSSolver(error_threshold=error_threshold, drop_path_p=0.0)
     compiled_solver = torch.compile(solver)
     result = compiled_solver(initial_guess, square_error)
     assert torch.isclose(result, torch.zeros_like(result), atol=error_threshold).all()
+    assert result.requires_grad
 
 
 class DemoWolfeConditionsModule(Module):

@@ -2,12 +2,14 @@
 # A/B one bench configuration under different environment settings of the same library
 # (e.g. DAVA_LDS_HISTORY, DAVA_LIB), one after another in one process each.
 # usage: tools/ab_env.sh "TAG:VAR=VAL [VAR=VAL ...]" ... ; extra bench args via BENCH_ARGS
+# "@BUILD@" in a value expands to the library's build/ directory (A/B variants: build/var_NAME/).
 set -uo pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 for spec in "$@"; do
   tag=${spec%%:*}
   envs=${spec#*:}
   [ "$envs" = "$spec" ] && envs=""
+  envs=${envs//@BUILD@/$R/deep-attention-visual-odometry_amd/build}
   out=$(env $envs timeout -k 10 300 python3 "$R/bench.py" --cpu-sample 0 ${BENCH_ARGS:---steps 3 --warmup 1} 2>&1 | tail -1) || {
     echo "$tag FAILED: $out"; exit 1; }
   echo "$tag $(echo "$out" | python3 -c 'import sys,json; d=json.loads(sys.stdin.read()); r=d["roofline"] or {}; g=d["diagnostics"]; print(d["value"], d["ms_per_step"], r.get("achieved"), r.get("frac"), g["objective_evals_per_iteration"], g.get("mean_steps_per_problem"), g["plan"])')"

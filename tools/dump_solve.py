@@ -30,6 +30,12 @@ def dump(path):
                 x, _, _ = native_ops.ba_solve(x0, obs, vis, m, n, False, iterations=k, error_threshold=-1.0,
                                               minimum_step=-1.0, hessian_mode=mode)
                 out[f"{case}_m{mode}_k{k}"] = x.cpu().numpy()
+    s = make_scenes(64, 2, 128, seed=4243)
+    x0, obs, vis = (torch.tensor(a, device=dev) for a in (s.initial, s.observations, s.visibility))
+    for k in (20, 100):
+        x, _, _ = native_ops.ba_solve(x0, obs, vis, 2, 128, False, iterations=k, error_threshold=-1.0,
+                                      minimum_step=-1.0, hessian_mode=1)
+        out[f"c2b64_k{k}"] = x.cpu().numpy()
     s = make_scenes(64, 4, 256, distortion=True, seed=4242)
     x0 = torch.tensor(s.initial, device=dev)
     obs = torch.tensor(s.observations, device=dev)
@@ -45,16 +51,20 @@ def dump(path):
 
 
 def compare(a, b):
+    """Prints one line per case; exit status 1 unless every case is bitwise identical."""
     za, zb = np.load(a), np.load(b)
+    all_same = True
     for k in za.files:
         x, y = za[k].astype(np.float64), zb[k].astype(np.float64)
         same = np.array_equal(za[k], zb[k])
+        all_same &= same
         rel = np.linalg.norm(x - y, axis=-1) / np.linalg.norm(y, axis=-1)
         print(f"{k:16s} bitwise={same} max_rel={rel.max():.2e}")
+    return all_same
 
 
 if __name__ == "__main__":
     if sys.argv[1] == "--compare":
-        compare(sys.argv[2], sys.argv[3])
+        sys.exit(0 if compare(sys.argv[2], sys.argv[3]) else 1)
     else:
         dump(sys.argv[1])
