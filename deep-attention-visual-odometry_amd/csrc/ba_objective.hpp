@@ -527,10 +527,20 @@ __device__ __forceinline__ bool ba_eval(const Layout& L, const S* x, const S* d,
     }
     if constexpr (GRAD) {
       if (m > 0) {
+        if constexpr (std::is_same<S, float>::value && DAVA_TRANSPOSED_SUMS) {
+          float w[7];
 #pragma unroll
-        for (int k = 0; k < 7; ++k) {
-          const S w = wave_sum(vg[k]);
-          if (lane == 0) vpart[(m * NW + wave) * kViewPart + k] = w;
+          for (int k = 0; k < 7; ++k) w[k] = vg[k];
+          wave_sums<7>(w);  // transposed: two wave_sum4 instead of seven wave_sum
+#pragma unroll
+          for (int k = 0; k < 7; ++k)
+            if (lane == 0) vpart[(m * NW + wave) * kViewPart + k] = w[k];
+        } else {
+#pragma unroll
+          for (int k = 0; k < 7; ++k) {
+            const S w = wave_sum(vg[k]);
+            if (lane == 0) vpart[(m * NW + wave) * kViewPart + k] = w;
+          }
         }
         // scale path, translation part: sum_m g_t~ . t (this thread's share) joins gsx in the
         // final block reduction

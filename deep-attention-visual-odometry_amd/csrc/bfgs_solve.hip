@@ -114,6 +114,19 @@ __host__ __device__ inline LdsCarve carve_lds(int M, int N, int Pv, int kcap = 0
 }
 
 typedef float f4v __attribute__((ext_vector_type(4)));
+typedef float f2v __attribute__((ext_vector_type(2)));
+
+#ifndef DAVA_PACKED_HISTORY
+#define DAVA_PACKED_HISTORY 1  // 0: the round-1 history arithmetic (per-element products, wave_sum per dot)
+#endif
+// packed fp32 FMA (v_pk_fma_f32): a * b + c on two lanes of a float pair
+__device__ __forceinline__ f2v pk_fma(f2v a, f2v b, f2v c) { return __builtin_elementwise_fma(a, b, c); }
+// k * v + c on a float4 as two packed FMAs
+__device__ __forceinline__ f4v pk_fma4(float k, f4v v, f4v c) {
+  const f2v kk = {k, k};
+  const f2v lo = pk_fma(kk, v.lo, c.lo), hi = pk_fma(kk, v.hi, c.hi);
+  return f4v{lo.x, lo.y, hi.x, hi.y};
+}
 
 __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
 __device__ __forceinline__ void st4(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
@@ -496,7 +509,24 @@ __device__ __forceinline__ void compact_products_fused(int P, int Pv, int nh, co
     const float4 t = ld4(g + 4 * q), u = ld4(gp + 4 * q);
     return f4v{t.x - u.x, t.y - u.y, t.z - u.z, t.w - u.w};
   };
+  // One entry: its four dots with y and g (per lane: packed 2-wide FMA chains, v_pk_fma_f32),
+  // one transposed wave reduction of the four (wave_sum4: uniform results), then the entry's
+  // contribution to H y and H g as packed FMAs.  ~90 VALU ops per entry at GM = 4 (the round-1
+  // form, per-element products + one wave_sum per dot: ~210).
   auto consume = [&](int j, const f4v (&s4)[GM], const f4v (&w4)[GM]) {
+#if DAVA_PACKED_HISTORY
+    f2v sy2 = {0.f, 0.f}, wy2 = {0.f, 0.f}, sg2 = {0.f, 0.f}, wg2 = {0.f, 0.f};
+#pragma unroll
+    for (int m = 0; m < GM; ++m) {
+      const f4v y = yvec(m), gm = gvec(m);
+      sy2 = pk_fma(s4[m].lo, y.lo, sy2); sy2 = pk_fma(s4[m].hi, y.hi, sy2);
+      wy2 = pk_fma(w4[m].lo, y.lo, wy2); wy2 = pk_fma(w4[m].hi, y.hi, wy2);
+      sg2 = pk_fma(s4[m].lo, gm.lo, sg2); sg2 = pk_fma(s4[m].hi, gm.hi, sg2);
+      wg2 = pk_fma(w4[m].lo, gm.lo, wg2); wg2 = pk_fma(w4[m].hi, gm.hi, wg2);
+    }
+    const float4 t = wave_sum4(sy2.x + sy2.y, wy2.x + wy2.y, sg2.x + sg2.y, wg2.x + wg2.y);
+    const float sy = t.x, wy = t.y, sg = t.z, wg = t.w;
+#else
     float sy = 0.f, wy = 0.f, sg = 0.f, wg = 0.f;
 #pragma unroll
     for (int m = 0; m < GM; ++m) {
@@ -508,12 +538,22 @@ __device__ __forceinline__ void compact_products_fused(int P, int Pv, int nh, co
       wg += (e[0] + e[1]) + (e[2] + e[3]);
     }
     sy = wave_sum(sy); wy = wave_sum(wy); sg = wave_sum(sg); wg = wave_sum(wg);
+#endif
+    // coefficients with the FMA written out: both call sites (LDS- and HBM-resident entries) must
+    // round them identically, and left to itself the compiler contracted cr sy - rho wy into an
+    // FMA at one site and not the other (hip's __fmul_rn / __fsub_rn do not stop contraction)
     const float rho = hrho[j], cr = hc[j] * rho;
-    const float ay = cr * sy - rho * wy, by = -rho * sy, ag = cr * sg - rho * wg, bg = -rho * sg;
+    const float ay = fmaf(cr, sy, -(rho * wy)), by = -rho * sy;
+    const float ag = fmaf(cr, sg, -(rho * wg)), bg = -rho * sg;
 #pragma unroll
     for (int m = 0; m < GM; ++m) {
+#if DAVA_PACKED_HISTORY
+      pa[m] = pk_fma4(by, w4[m], pk_fma4(ay, s4[m], pa[m]));
+      pb[m] = pk_fma4(bg, w4[m], pk_fma4(ag, s4[m], pb[m]));
+#else
       pa[m] += ay * s4[m] + by * w4[m];
       pb[m] += ag * s4[m] + bg * w4[m];
+#endif
     }
   };
   auto load = [&](int j, f4v (&s4)[GM], f4v (&w4)[GM]) {

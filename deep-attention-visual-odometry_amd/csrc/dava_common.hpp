@@ -48,6 +48,45 @@ __device__ __forceinline__ float wave_sum<float>(float v) {
   return __uint_as_float(q[0]) + __uint_as_float(q[1]);  // xor 32
 }
 
+__device__ __forceinline__ float lane_value(float v, int lane) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane));
+}
+
+// Sums of FOUR per-lane values over the wave, returned wave-uniform (read out of fixed lanes, so
+// SGPR-resident and bit-identical for every lane).  A transposed butterfly: the xor-32 step
+// exchanges half of the value SET between the lane halves (v0, v1 stay low, v2, v3 go high) and
+// the xor-16 step half of what is left, so each 16-lane row ends up reducing ONE value with four
+// DPP steps -- 14 VALU ops for the four sums instead of 4 x 8 for four wave_sum calls.
+// (v_permlane32_swap: lanes 32-63 of the first operand <-> lanes 0-31 of the second;
+//  v_permlane16_swap: odd rows of the first <-> even rows of the second.)
+__device__ __forceinline__ float4 wave_sum4(float v0, float v1, float v2, float v3) {
+  const auto a = __builtin_amdgcn_permlane32_swap(__float_as_uint(v0), __float_as_uint(v2), false, false);
+  const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v1), __float_as_uint(v3), false, false);
+  const float h0 = __uint_as_float(a[0]) + __uint_as_float(a[1]);  // lanes 0-31: v0, lanes 32-63: v2
+  const float h1 = __uint_as_float(b[0]) + __uint_as_float(b[1]);  // lanes 0-31: v1, lanes 32-63: v3
+  const auto c = __builtin_amdgcn_permlane16_swap(__float_as_uint(h0), __float_as_uint(h1), false, false);
+  float r = __uint_as_float(c[0]) + __uint_as_float(c[1]);  // 16-lane row q holds value q
+  r += dpp_mov<0xB1>(r);
+  r += dpp_mov<0x4E>(r);
+  r += dpp_mov<0x141>(r);
+  r += dpp_mov<0x140>(r);
+  return make_float4(lane_value(r, 0), lane_value(r, 16), lane_value(r, 32), lane_value(r, 48));
+}
+
+// Wave sums of R values in place (wave-uniform results), four at a time through wave_sum4.
+template <int R>
+__device__ __forceinline__ void wave_sums(float (&v)[R]) {
+#pragma unroll
+  for (int r = 0; r < R; r += 4) {
+    const float4 t = wave_sum4(v[r], r + 1 < R ? v[r + 1] : 0.f, r + 2 < R ? v[r + 2] : 0.f,
+                               r + 3 < R ? v[r + 3] : 0.f);
+    v[r] = t.x;
+    if (r + 1 < R) v[r + 1] = t.y;
+    if (r + 2 < R) v[r + 2] = t.z;
+    if (r + 3 < R) v[r + 3] = t.w;
+  }
+}
+
 // Deterministic block-wide sum of R values: wave butterflies, then the 4 wave
 // partials are added in a fixed order by every thread, so all threads hold
 // bit-identical results (the solver's control flow depends on them being
@@ -55,15 +94,28 @@ __device__ __forceinline__ float wave_sum<float>(float v) {
 // so ONE barrier per reduction suffices (NW = waves in the workgroup): a wave cannot reach the next use of
 // the same buffer before every wave has passed the intervening reduction's
 // barrier, i.e. before every wave finished reading this one.
+#ifndef DAVA_TRANSPOSED_SUMS
+#define DAVA_TRANSPOSED_SUMS 1  // 0: one wave_sum per value (the round-1 form)
+#endif
 template <int R, int NW = kWaves>
 __device__ __forceinline__ void block_sum(float (&v)[R], float* scratch, int buf) {
   const int lane = threadIdx.x & (kWave - 1);
   const int wave = threadIdx.x / kWave;
   float* s = scratch + buf * (NW * 32);
+  if constexpr (DAVA_TRANSPOSED_SUMS && R >= 2) {
+    float w[R];
 #pragma unroll
-  for (int r = 0; r < R; ++r) {
-    float w = wave_sum(v[r]);
-    if (lane == 0) s[wave * 32 + r] = w;
+    for (int r = 0; r < R; ++r) w[r] = v[r];
+    wave_sums<R>(w);
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+      if (lane == 0) s[wave * 32 + r] = w[r];
+  } else {
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      float w = wave_sum(v[r]);
+      if (lane == 0) s[wave * 32 + r] = w;
+    }
   }
   __syncthreads();
 #pragma unroll

@@ -1,7 +1,7 @@
 #!/bin/bash
 # One parameterised GPU-box session (run via gpurun from the repo root).  Each argument is a step,
 # run in order; the first failing step ends the session (no GPU step runs after a failure).
-#   tests[=PYTEST_ARGS]   pytest -m gpu (default: the whole suite)
+#   tests[=PYTEST_ARGS]   pytest -m gpu (default: the whole suite); e.g. 'tests=-k "golden or headline"' 
 #   smoke                 __graft_entry__.smoke()
 #   bench[=BENCH_ARGS]    python bench.py (default flags) -> gpurun_out/bench.log
 #   configs               tools/measure_configs.sh (one bench line per configuration)
@@ -22,7 +22,8 @@ for s in "$@"; do
   case $name in
     tests)
       step tests "$val"
-      timeout -k 10 1000 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread ${val} \
+      # PYTEST_ARGS may quote a -k expression: tests='-k "a or b"'
+      eval "timeout -k 10 1000 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread ${val}" \
         > gpurun_out/tests.log 2>&1
       rc=$?; grep -E "passed|failed|error" gpurun_out/tests.log | tail -3
       [ $rc -eq 0 ] || { grep -E "FAILED|Error" gpurun_out/tests.log | head -20; exit $rc; } ;;
