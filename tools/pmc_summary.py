@@ -58,8 +58,11 @@ def main():
         json.dump(summary, fh, indent=2)
     tj_path = os.path.join(dst, "pmc_traffic.json")
     tj = json.load(open(tj_path)) if os.path.exists(tj_path) else {}
+    import datetime
+
     tj[key] = {"tag": tag, "hbm_bytes_per_launch": summary["hbm_bytes_per_launch"],
-               "avg_duration_ms": summary["avg_duration_ms"]}
+               "avg_duration_ms": summary["avg_duration_ms"],
+               "date": datetime.date.today().isoformat()}
     with open(tj_path, "w") as fh:
         json.dump(tj, fh, indent=2, sort_keys=True)
     print(json.dumps(summary, indent=2))
