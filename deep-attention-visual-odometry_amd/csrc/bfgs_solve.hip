@@ -674,7 +674,7 @@ __device__ __forceinline__ void compact_products_fused(int P, int Pv, int nh, co
 template <int MODE, bool GV, int RES, bool XL, int PPT, int NW>
 __global__ __launch_bounds__(kWave * NW, DAVA_SOLVE_WAVES_PER_EU) void bfgs_ba_solve_kernel(SolveArgs a) {
   static_assert(!XL || GV, "XL is a global-vector-mode variant");
-  static_assert(GV ? NW == solve_waves(true) : (NW == 2 || NW == 4), "LDS mode runs 2- or 4-wave workgroups");
+  static_assert(GV ? NW == solve_waves(true) : (NW == 1 || NW == 2 || NW == 4), "LDS mode runs 1-, 2- or 4-wave workgroups");
   constexpr int BLOCK = kWave * NW;
   extern __shared__ __attribute__((aligned(16))) float lds[];
 #if DAVA_BASE_PRIO
@@ -826,7 +826,7 @@ __global__ __launch_bounds__(kWave * NW, DAVA_SOLVE_WAVES_PER_EU) void bfgs_ba_s
   #ifndef DAVA_COMPACT_TWO_PASS
             const int G4 = (P + 3) / 4;
             const int GM = (G4 + kWave - 1) / kWave;
-            deferred = DAVA_DEFER_COMBINE && !GV && GM <= 4;
+            deferred = DAVA_DEFER_COMBINE && !GV && NW > 1 && GM <= 4;
             if constexpr (GV) {  // workgroup-wide single pass, else two passes
               const int GT = (G4 + kWave * NW - 1) / (kWave * NW);
               const int nh = k - 1;
@@ -1115,17 +1115,26 @@ static int lds_bytes_for(const DavaScene* s, int kcap = 0, bool gv = false, int 
          DAVA_EXTRA_LDS;
 }
 
-// Waves per LDS-mode workgroup (GV mode: always 8).  Four by default; DAVA_SOLVE_WAVES=2|4
-// overrides (A/B and tests).
-static int lds_mode_waves(const DavaScene* s) {
-  (void)s;
+// Waves per LDS-mode workgroup (GV mode: always 8).  The register budget (256 VGPRs) holds two
+// waves per SIMD, eight per CU, whatever the split, so the choice is how many waves share one
+// problem: two waves while a history row is at most 2 x 64 float4 column groups (P <= 512), else
+// four, so small problems do not pay for barriers and cross-wave sums over idle waves
+// (interleaved A/B, profiles/r02_ab_waves.log: C2 +19%, 8192 two-view 64-point problems +49%,
+// C3 -17% at two).  One wave per problem measured another +9% on the 64-point shape but put one
+// K = 100 run-to-stagnation problem 3e-5 from the oracle (30x the reference's own 1-ulp
+// sensitivity), so it stays opt-in.  DENSE keeps 4.  DAVA_SOLVE_WAVES=1|2|4 overrides (A/B, tests).
+static int lds_mode_waves(const DavaScene* s, int mode) {
   if (const char* e = getenv("DAVA_SOLVE_WAVES")) {
     const int w = atoi(e);
-    if (w == 2 || w == 4) return w;
+    if (w == 1 || w == 2 || w == 4) return w;
   }
-  return 4;
+  if (mode != DAVA_HESSIAN_COMPACT) return 4;
+  const int groups = (round_up(s->num_parameters, 4) / 4 + kWave - 1) / kWave;  // per-lane float4 groups at 1 wave
+  return groups <= 2 ? 2 : 4;
 }
-static int solve_waves_for(const DavaScene* s, bool gv) { return gv ? solve_waves(true) : lds_mode_waves(s); }
+static int solve_waves_for(const DavaScene* s, bool gv, int mode) {
+  return gv ? solve_waves(true) : lds_mode_waves(s, mode);
+}
 
 // Global-vector mode when the all-in-LDS image would cost more than two workgroups
 // per CU (e.g. C5: P = 12381 -> 446 KB of vectors per problem).
@@ -1166,7 +1175,8 @@ static int lds_history_entries(const DavaScene* s, int kcap, bool gv, int nw) {
   if (gv || kcap <= 0 || (Pv / 4 + kWave - 1) / kWave > 4) return 0;
   const int base = lds_bytes_for(s, kcap, false, 0, false, nw);
   const int per = 2 * Pv * (int)sizeof(float);
-  const int per_cu = 4 * DAVA_SOLVE_WAVES_PER_EU / nw;  // workgroups per CU at the register limit
+  int per_cu = 4 * DAVA_SOLVE_WAVES_PER_EU / nw;  // workgroups per CU at the register limit
+  if (const char* e = getenv("DAVA_WG_PER_CU")) per_cu = max(1, atoi(e));  // A/B knob: LDS budget = 160 KB / this
   int n = (kMaxLds / per_cu - base) / per;
   if (const char* e = getenv("DAVA_LDS_HISTORY")) n = atoi(e);
   n = min(n, (kMaxLds - base) / per);
@@ -1201,7 +1211,7 @@ extern "C" int dava_ba_solve_plan(const DavaScene* scene, const DavaSolverConfig
   if (mode != DAVA_HESSIAN_DENSE && mode != DAVA_HESSIAN_COMPACT) return DAVA_ERR_INVALID_ARGUMENT;
   const int kcap = mode == DAVA_HESSIAN_COMPACT ? compact_capacity(config) : 0;
   const bool gv = use_gv(scene, kcap);
-  const int nw = solve_waves_for(scene, gv);
+  const int nw = solve_waves_for(scene, gv, mode);
   const int lcap = mode == DAVA_HESSIAN_COMPACT ? lds_history_entries(scene, kcap, gv, nw) : 0;
   plan->global_vectors = gv ? 1 : 0;
   plan->workgroup_threads = kWave * nw;
@@ -1243,12 +1253,13 @@ static void launch_solve_ppt(const SolveArgs& a, int B, int lds, hipStream_t s) 
 // N <= 256; C3 +12% over re-reading x, d and the gradient from LDS per view).  Larger N, GV
 // mode and DAVA_NO_PPT take the re-reading variant: eight points per thread at C5 spill
 // (1 KB of scratch per lane) and ran 42% slower.
-template <bool GV, bool XL>
-constexpr int kRegisterPoints = GV ? 0 : 1;
+// One-wave workgroups (one problem per wave) hold two points per lane (N <= 128).
+template <bool GV, bool XL, int NW>
+constexpr int kRegisterPoints = GV ? 0 : (NW == 1 ? 2 : 1);
 
 template <int MODE, bool GV, int RES, bool XL, int NW>
 static void launch_solve_nw(const SolveArgs& a, int B, int lds, hipStream_t s) {
-  constexpr int R = kRegisterPoints<GV, XL>;
+  constexpr int R = kRegisterPoints<GV, XL, NW>;
   if (R > 0 && a.L.N <= R * kWave * NW && getenv("DAVA_NO_PPT") == nullptr)
     launch_solve_ppt<MODE, GV, RES, XL, R, NW>(a, B, lds, s);
   else
@@ -1258,6 +1269,7 @@ static void launch_solve_nw(const SolveArgs& a, int B, int lds, hipStream_t s) {
 template <int MODE, bool GV, int RES, bool XL>
 static void launch_solve_res(const SolveArgs& a, int B, int lds, hipStream_t s, int nw) {
   if constexpr (GV) launch_solve_nw<MODE, GV, RES, XL, solve_waves(true)>(a, B, lds, s);
+  else if (nw == 1) launch_solve_nw<MODE, GV, RES, XL, 1>(a, B, lds, s);
   else if (nw == 2) launch_solve_nw<MODE, GV, RES, XL, 2>(a, B, lds, s);
   else launch_solve_nw<MODE, GV, RES, XL, 4>(a, B, lds, s);
 }
@@ -1282,7 +1294,7 @@ extern "C" int dava_ba_solve(const DavaScene* scene, const DavaSolverConfig* con
   if (kcap > kMaxCompactEntries) return DAVA_ERR_UNSUPPORTED;
   const bool gv = use_gv(scene, kcap);
   const bool xl = use_xl(scene, kcap, gv);
-  const int nw = solve_waves_for(scene, gv);
+  const int nw = solve_waves_for(scene, gv, mode);
   const int lcap = mode == DAVA_HESSIAN_COMPACT ? lds_history_entries(scene, kcap, gv, nw) : 0;
   const int lds = lds_bytes_for(scene, kcap, gv, lcap, xl, nw);
   if (lds > kMaxLds) return DAVA_ERR_UNSUPPORTED;

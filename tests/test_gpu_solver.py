@@ -356,6 +356,27 @@ def test_work_queue_launch_is_bitwise_invisible(device, stopping, monkeypatch):
         assert st[:, 0].unique().numel() > 1
 
 
+@pytest.mark.parametrize("waves", ["1", "2", "4"])
+@pytest.mark.parametrize("m,n,distortion,k", [(2, 64, False, 20), (2, 128, False, 20), (4, 256, True, 20)])
+def test_workgroup_waves_match_oracle(device, m, n, distortion, k, waves, monkeypatch):
+    """One problem per 1-, 2- or 4-wave workgroup (DAVA_SOLVE_WAVES; the plan picks one per
+    shape): the reduction trees differ, the parity bar against the oracle does not."""
+    from deep_attention_visual_odometry_amd import native_ops
+
+    x0, obs, vis = _scene(8, m, n, distortion, 600 + n + k)
+    kw = dict(iterations=k, error_threshold=-1.0, minimum_step=-1.0)
+    ref = solver.bfgs_solve(x0, objective.ReprojectionClosure(obs, vis, m, n, distortion), **kw)
+    monkeypatch.setenv("DAVA_SOLVE_WAVES", waves)
+    assert native_ops.solve_plan(8, m, n, distortion, 1, k)["workgroup_threads"] == 64 * int(waves)
+    for mode in ("compact", "dense"):
+        out, status = _gpu_solve(device, x0, obs, vis, m, n, distortion, hessian_mode=mode, **kw)
+        rel = _rel(out, ref)
+        _report(f"waves{waves}_{mode}_M{m}_N{n}_D{int(distortion)}_K{k}_B8", rel)
+        assert rel.max() <= TOL, (mode, rel)
+        assert (status[:, 0] == k).all()
+    monkeypatch.delenv("DAVA_SOLVE_WAVES")
+
+
 @pytest.mark.parametrize("m,n,distortion", [(4, 256, True), (2, 128, False)])
 def test_lds_resident_history_is_bitwise_invisible(device, m, n, distortion, monkeypatch):
     """COMPACT mode keeps the oldest history entries on-chip (dava_ba_solve_plan); the products

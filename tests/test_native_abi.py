@@ -95,6 +95,13 @@ def test_solve_plan(lib, monkeypatch):
     assert native_ops.solve_plan(8192, 4, 256, True, 0, 100)["lds_history_entries"] == 0  # dense
     c5 = native_ops.solve_plan(256, 16, 4096, False, 1, 100)
     assert c5["global_vectors"] == 1 and c5["workgroup_threads"] == 512 and c5["lds_history_entries"] == 0
+    # two waves while a history row is at most 128 float4 column groups: C1 (P = 201), C2 (P = 393)
+    monkeypatch.delenv("DAVA_SOLVE_WAVES", raising=False)
+    assert native_ops.solve_plan(1024, 2, 64, False, 1, 100)["workgroup_threads"] == 128
+    assert native_ops.solve_plan(1024, 2, 128, False, 1, 100)["workgroup_threads"] == 128
+    assert native_ops.solve_plan(1024, 2, 128, False, 0, 100)["workgroup_threads"] == 256  # dense keeps 4
+    monkeypatch.setenv("DAVA_SOLVE_WAVES", "4")
+    assert native_ops.solve_plan(1024, 2, 64, False, 1, 100)["workgroup_threads"] == 256
     monkeypatch.setenv("DAVA_LDS_HISTORY", "1000")  # clamped to one workgroup's LDS
     big = native_ops.solve_plan(8192, 4, 256, True, 1, 100)
     assert big["lds_bytes"] <= 160 * 1024 and big["lds_history_entries"] > c3["lds_history_entries"]
