@@ -1,0 +1,436 @@
+// Reverse mode of the fused compact BFGS solve: d x_out / d (x0, observations) applied to a
+// cotangent, one workgroup per problem, replaying the recorded solve (dava_tape.hpp) backwards.
+//
+// Replaces, for the fused objectives, differentiating THROUGH BFGSSolver.forward the way the
+// reference does (create_graph, autograd_solvers/bfgs_solver.py:85, :133-135, :213-215): every
+// iteration's gradient is taken with create_graph, the inverse-Hessian scale and update
+// (:159-180, :217-303, utils/func_inverse_curvature.py:21-51) and d = -H g are differentiated, the
+// step size of the line search is a constant (it is computed without a graph).
+//
+// Forward (per problem, k = 0 .. n-1, n = the steps the solve took):
+//   g_k = dE/dx(x_k; obs)            d_0 = -g_0,   d_k = -H_k g_k
+//   H_k = H_{k-1} + c rho s s^T - rho s w^T - rho w s^T   (entry k-1: s = s_{k-1}, y = g_k - g_{k-1},
+//         w = H_{k-1} y, rho = 1 / (s.y) (0 if s.y <= 0), c = 1 + rho y.w),  H_0' = gamma I,
+//         gamma = clamp(s_0.y_1 / clamp(y_1.y_1, 1e-5), min 1e-4)
+//   s_k = alpha_k d_k,  x_{k+1} = x_k + s_k
+// Reverse, with A = adjoint of H_k kept as a sum of outer products sum_j a_j g_j^T: every term the
+// forward adds to the adjoint of an inverse Hessian is -dbar_j g_j^T (from d_j = -H_j g_j) or
+// wbar_j y_j^T = wbar_j (g_j - g_{j-1})^T (from w_j = H_{j-1} y_j), so ONE row a_j per iteration
+// holds all of them (rows a_j in the workspace, g_j in the tape).  Only the symmetric part of A
+// is ever contracted (s^T A s, (A + A^T) s, (A + A^T) w, tr A), so the reference's separate
+// y^T H / H y products need no separate treatment.  Step k:
+//   sbar = xbar + sbar_pend,  dbar = alpha_k sbar
+//   k >= 1:  a_k -= dbar;  P1 = (A + A^T) s,  P2 = (A + A^T) w   (one pass over a_j, g_j, j >= k)
+//            cbar = rho s.P1 / 2,  rhobar = c s.P1 / 2 - s.P2 + cbar y.w,  tbar = -rho^2 rhobar (s.y > 0)
+//            sbar_pend' = c rho P1 - rho P2 + tbar y,  wbar = -rho P1 + cbar rho y
+//            ybar = cbar rho w + tbar s + H_{k-1} wbar
+//            gbar_k = gbar_pend - H_k dbar + ybar,  gbar_pend' = -ybar,  a_k += wbar,  a_{k-1} = -wbar
+//            k = 1: gammabar = tr A = sum_j a_j . g_j, through both clamps into s_0 and y_1
+//   k = 0:   gbar_0 = gbar_pend - dbar
+//   xbar += Hess E(x_k) gbar_k,  obsbar += (d2E / dobs dx) gbar_k    (forward-over-reverse, Dual)
+// H_k dbar and H_{k-1} wbar come from one pass over the history rows (s_j, w_j), like the forward's.
+#include "ba_objective.hpp"
+#include "dava_tape.hpp"
+
+namespace dava {
+
+typedef float f4a __attribute__((ext_vector_type(4)));
+
+struct AdjointArgs {
+  Layout L;
+  int Pv, K;
+  TapeLayout tl;
+  const float* tape;
+  const float* obs;
+  const uint8_t* vis;
+  const int32_t* status;
+  const float* xbar;  // (B, P) cotangent of x_out
+  float* x0_grad;     // (B, P)
+  float* obs_grad;    // (B, M, N, 2) or null
+  float* arows;       // (B, K, Pv) workspace
+};
+
+constexpr int kAdjWaves = 4;
+constexpr int kAdjBlock = kWave * kAdjWaves;
+
+struct AdjointCarve {
+  int xb, sbp, gbp, db, gk, p1, p2, wb, hd, hw, sv, wv, yv, gv, sp0, sp1, sp2, sp3, sc, xd, gd, views, vpart, obsd,
+      obs, obsacc, scratch, vis_bytes_off, total_bytes;
+};
+
+__host__ __device__ inline AdjointCarve carve_adjoint(int M, int N, int Pv, int T) {
+  AdjointCarve c;
+  int off = 0;
+  int* vec[] = {&c.xb, &c.sbp, &c.gbp, &c.db, &c.gk, &c.p1, &c.p2, &c.wb, &c.hd, &c.hw,
+                &c.sv, &c.wv, &c.yv, &c.gv, &c.sp0, &c.sp1, &c.sp2, &c.sp3};
+  for (int* v : vec) { *v = off; off += Pv; }
+  c.sc = off; off += T;
+  c.xd = off; off += 2 * Pv;  // Dual
+  c.gd = off; off += 2 * Pv;  // Dual
+  c.views = off; off += 2 * round_up(views_floats(M), 4);
+  c.vpart = off; off += 2 * round_up(vpart_floats(M, kAdjWaves), 4);
+  c.obsd = off; off += 2 * 2 * M * N;  // Dual dE/dobs per (view, point)
+  c.obs = off; off += round_up(2 * M * N, 4);
+  c.obsacc = off; off += round_up(2 * M * N, 4);
+  c.scratch = off; off += 2 * kAdjWaves * 32;
+  c.vis_bytes_off = off * 4;
+  c.total_bytes = c.vis_bytes_off + round_up(M * N, 16);
+  return c;
+}
+
+__device__ __forceinline__ f4a ldv(const float* p) { return *reinterpret_cast<const f4a*>(p); }
+__device__ __forceinline__ void stv(float* p, f4a v) { *reinterpret_cast<f4a*>(p) = v; }
+__device__ __forceinline__ float dot4(f4a a, f4a b) {
+  const f4a t = a * b;
+  return (t[0] + t[1]) + (t[2] + t[3]);
+}
+
+// One pass over entries j0 .. j1-1 with rows R1[j], R2[j] (Pv floats, rows Pv apart): per entry the
+// four dots d11 = R1.v1, d21 = R2.v1, d12 = R1.v2, d22 = R2.v2 (one transposed wave reduction),
+// then out1 += k1 R1 + k2 R2, out2 += k3 R1 + k4 R2 with (k1..k4) = coef(j, d11, d21, d12, d22).
+// Entries are dealt round-robin to the 4 waves (two in flight per wave); the wave partials are added
+// in the fixed order (w0 + w2) + (w1 + w3), then base * (v1 | v2).  out / v / spares: LDS vectors.
+// Ends with a barrier.
+template <int GM, class Coef>
+__device__ __forceinline__ void pair_pass(int P, int Pv, int j0, int j1, const float* __restrict__ R1,
+                                          const float* __restrict__ R2, const float* v1, const float* v2,
+                                          float base, Coef coef, float* out1, float* out2, float* sp0, float* sp1,
+                                          float* sp2, float* sp3) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wave = threadIdx.x / kWave;
+  const int G = (P + 3) / 4;
+  f4a pa[GM], pb[GM];
+  bool ok[GM];
+#pragma unroll
+  for (int m = 0; m < GM; ++m) {
+    ok[m] = lane + kWave * m < G;
+    pa[m] = pb[m] = f4a{0, 0, 0, 0};
+  }
+  auto load = [&](int j, f4a (&r1)[GM], f4a (&r2)[GM]) {
+#pragma unroll
+    for (int m = 0; m < GM; ++m) {
+      const int q = lane + kWave * m;
+      r1[m] = ok[m] ? ldv(R1 + (size_t)j * Pv + 4 * q) : f4a{0, 0, 0, 0};
+      r2[m] = ok[m] ? ldv(R2 + (size_t)j * Pv + 4 * q) : f4a{0, 0, 0, 0};
+    }
+  };
+  auto consume = [&](int j, const f4a (&r1)[GM], const f4a (&r2)[GM]) {
+    float d11 = 0.f, d21 = 0.f, d12 = 0.f, d22 = 0.f;
+#pragma unroll
+    for (int m = 0; m < GM; ++m) {
+      const int q = lane + kWave * m;
+      const f4a a = ok[m] ? ldv(v1 + 4 * q) : f4a{0, 0, 0, 0};
+      const f4a c = ok[m] ? ldv(v2 + 4 * q) : f4a{0, 0, 0, 0};
+      d11 += dot4(r1[m], a);
+      d21 += dot4(r2[m], a);
+      d12 += dot4(r1[m], c);
+      d22 += dot4(r2[m], c);
+    }
+    const float4 t = wave_sum4(d11, d21, d12, d22);
+    float k1, k2, k3, k4;
+    coef(j, t.x, t.y, t.z, t.w, k1, k2, k3, k4);
+#pragma unroll
+    for (int m = 0; m < GM; ++m) {
+      pa[m] += k1 * r1[m] + k2 * r2[m];
+      pb[m] += k3 * r1[m] + k4 * r2[m];
+    }
+  };
+  int j = j0 + wave;
+  for (; j + kAdjWaves < j1; j += 2 * kAdjWaves) {
+    f4a r1a[GM], r2a[GM], r1b[GM], r2b[GM];
+    load(j, r1a, r2a);
+    load(j + kAdjWaves, r1b, r2b);
+    consume(j, r1a, r2a);
+    consume(j + kAdjWaves, r1b, r2b);
+  }
+  for (; j < j1; j += kAdjWaves) {
+    f4a r1[GM], r2[GM];
+    load(j, r1, r2);
+    consume(j, r1, r2);
+  }
+  auto put = [&](float* A, float* B) {
+#pragma unroll
+    for (int m = 0; m < GM; ++m)
+      if (ok[m]) {
+        const int q = lane + kWave * m;
+        stv(A + 4 * q, pa[m]);
+        stv(B + 4 * q, pb[m]);
+      }
+  };
+  auto add = [&](const float* A, const float* B) {
+#pragma unroll
+    for (int m = 0; m < GM; ++m)
+      if (ok[m]) {
+        const int q = lane + kWave * m;
+        pa[m] += ldv(A + 4 * q);
+        pb[m] += ldv(B + 4 * q);
+      }
+  };
+  if (wave == 2) put(sp0, sp1);
+  if (wave == 3) put(sp2, sp3);
+  __syncthreads();
+  if (wave == 0) add(sp0, sp1);
+  if (wave == 1) {
+    add(sp2, sp3);
+    put(sp2, sp3);
+  }
+  __syncthreads();
+  if (wave == 0) {
+    add(sp2, sp3);
+#pragma unroll
+    for (int m = 0; m < GM; ++m)
+      if (ok[m]) {
+        const int q = lane + kWave * m;
+        pa[m] += base * ldv(v1 + 4 * q);
+        pb[m] += base * ldv(v2 + 4 * q);
+      }
+    put(out1, out2);
+  }
+  __syncthreads();
+}
+
+template <int RES, int GM>
+__global__ __launch_bounds__(kAdjBlock, 1) void bfgs_ba_adjoint_kernel(AdjointArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const Layout L = a.L;
+  const int P = L.P, M = L.M, N = L.N, MN = M * N, Pv = a.Pv, K = a.K;
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const TapeLayout& tl = a.tl;
+  const AdjointCarve cv = carve_adjoint(M, N, Pv, tl.T);
+  float* xb = lds + cv.xb;    // xbar: adjoint of x_{k+1} entering step k, of x_k leaving it
+  float* sbp = lds + cv.sbp;  // adjoint of s_k from the update that used it (step k + 1)
+  float* gbp = lds + cv.gbp;  // adjoint of g_k from y_{k+1} = g_{k+1} - g_k
+  float* db = lds + cv.db;
+  float* gk = lds + cv.gk;
+  float* p1 = lds + cv.p1;
+  float* p2 = lds + cv.p2;
+  float* wb = lds + cv.wb;
+  float* hd = lds + cv.hd;
+  float* hw = lds + cv.hw;
+  float* sv = lds + cv.sv;
+  float* wv = lds + cv.wv;
+  float* yv = lds + cv.yv;
+  float* gv = lds + cv.gv;
+  float* sp0 = lds + cv.sp0;
+  float* sp1 = lds + cv.sp1;
+  float* sp2 = lds + cv.sp2;
+  float* sp3 = lds + cv.sp3;
+  float* sc = lds + cv.sc;
+  Dual* xd = reinterpret_cast<Dual*>(lds + cv.xd);
+  Dual* gd = reinterpret_cast<Dual*>(lds + cv.gd);
+  Dual* views = reinterpret_cast<Dual*>(lds + cv.views);
+  Dual* vpart = reinterpret_cast<Dual*>(lds + cv.vpart);
+  Dual* obsd = reinterpret_cast<Dual*>(lds + cv.obsd);
+  float* obs = lds + cv.obs;
+  float* obsacc = lds + cv.obsacc;
+  float* scratch = lds + cv.scratch;
+  uint8_t* vis = reinterpret_cast<uint8_t*>(lds) + cv.vis_bytes_off;
+
+  const float* S = a.tape + tl.hist + (size_t)b * 2 * tl.kcap * Pv;  // history rows s_j
+  const float* W = S + (size_t)tl.kcap * Pv;                          // w_j
+  const float* X = a.tape + tl.x + (size_t)b * K * Pv;
+  const float* Gr = a.tape + tl.g + (size_t)b * K * Pv;
+  float* Ar = a.arows + (size_t)b * K * Pv;
+
+  for (int i = tid; i < Pv; i += kAdjBlock) {
+    xb[i] = i < P ? a.xbar[(size_t)b * P + i] : 0.f;
+    sbp[i] = gbp[i] = 0.f;
+  }
+  for (int i = tid; i < tl.T; i += kAdjBlock) sc[i] = a.tape[tl.scal + (size_t)b * tl.T + i];
+  for (int i = tid; i < 2 * MN; i += kAdjBlock) {
+    obs[i] = a.obs[(size_t)b * 2 * MN + i];
+    obsacc[i] = 0.f;
+  }
+  for (int i = tid; i < MN; i += kAdjBlock) vis[i] = a.vis[(size_t)b * MN + i] ? 1 : 0;
+  const int n = min(a.status[(size_t)b * DAVA_STATUS_WORDS], K);
+  const float gamma = sc[3 * K];
+  float trace = 0.f;  // sum_{j > k} a_j . g_j with every a_j final (needed at k = 1: gamma's adjoint)
+  int buf = 0;
+  __syncthreads();
+
+  for (int k = n - 1; k >= 0; --k) {
+    const float alpha = sc[k];
+    // ---- s_k = alpha d_k, x_{k+1} = x_k + s_k (alpha is a constant of the line search) ----
+    for (int i = tid; i < Pv; i += kAdjBlock) db[i] = alpha * (xb[i] + sbp[i]);
+    if (k == 0) {
+      for (int i = tid; i < Pv; i += kAdjBlock) gk[i] = gbp[i] - db[i];  // d_0 = -g_0
+    } else {
+      const float* gk1 = Gr + (size_t)(k - 1) * Pv;
+      const float* gkr = Gr + (size_t)k * Pv;
+      const float* srow = S + (size_t)(k - 1) * Pv;
+      const float* wrow = W + (size_t)(k - 1) * Pv;
+      float* ak = Ar + (size_t)k * Pv;
+      for (int i = tid; i < Pv; i += kAdjBlock) {
+        const float g1 = i < P ? gkr[i] : 0.f, g0 = i < P ? gk1[i] : 0.f;
+        gv[i] = g1;
+        yv[i] = g1 - g0;
+        sv[i] = srow[i];
+        wv[i] = wrow[i];
+        ak[i] = (k == n - 1 ? 0.f : ak[i]) - db[i];  // d_k = -H_k g_k adds -dbar_k g_k^T to H_k's adjoint
+      }
+      __syncthreads();
+      const float rho = sc[K + k - 1], c = sc[2 * K + k - 1];
+      // P1 = (A + A^T) s, P2 = (A + A^T) w over rows (a_j, g_j), j = k .. n-1
+      pair_pass<GM>(P, Pv, k, n, Ar, Gr, sv, wv, 0.f,
+                    [](int, float as, float gs, float aw, float gw, float& k1, float& k2, float& k3, float& k4) {
+                      k1 = gs; k2 = as; k3 = gw; k4 = aw;
+                    },
+                    p1, p2, sp0, sp1, sp2, sp3);
+      float r[7] = {0, 0, 0, 0, 0, 0, 0};
+      for (int i = tid; i < P; i += kAdjBlock) {
+        const float si = sv[i], wi = wv[i], yi = yv[i], di = db[i];
+        r[0] += si * p1[i]; r[1] += si * p2[i]; r[2] += yi * wi; r[3] += si * di; r[4] += wi * di;
+        r[5] += yi * yi; r[6] += si * yi;
+      }
+      block_sum<7, kAdjWaves>(r, scratch, buf);
+      buf ^= 1;
+      const float sAs = 0.5f * r[0], sAw = r[1], yw = r[2], sd = r[3], wd = r[4], yy = r[5], t = r[6];
+      const float cbar = rho * sAs;
+      const float rhobar = c * sAs - sAw + cbar * yw;
+      const float tbar = rho > 0.f ? -(rho * rho) * rhobar : 0.f;  // inverse_curvature backward
+      for (int i = tid; i < Pv; i += kAdjBlock) {
+        const float q1 = p1[i], q2 = p2[i];
+        wb[i] = -rho * q1 + (cbar * rho) * yv[i];
+        p2[i] = (cbar * rho) * wv[i] + tbar * sv[i];  // ybar, direct terms
+        sbp[i] = (c * rho) * q1 - rho * q2 + tbar * yv[i];
+      }
+      __syncthreads();
+      // H_{k-1} dbar and H_{k-1} wbar: one pass over history entries 0 .. k-2, plus gamma I
+      if (k >= 2) {
+        const float* hrho = sc + K;
+        const float* hc = sc + 2 * K;
+        pair_pass<GM>(P, Pv, 0, k - 1, S, W, db, wb, gamma,
+                      [hrho, hc](int j, float sdv, float wdv, float swv, float wwv, float& k1, float& k2, float& k3,
+                                 float& k4) {
+                        const float rj = hrho[j], cr = hc[j] * rj;
+                        k1 = cr * sdv - rj * wdv; k2 = -rj * sdv;
+                        k3 = cr * swv - rj * wwv; k4 = -rj * swv;
+                      },
+                      hd, hw, sp0, sp1, sp2, sp3);
+      } else {
+        for (int i = tid; i < Pv; i += kAdjBlock) {
+          hd[i] = gamma * db[i];
+          hw[i] = gamma * wb[i];
+        }
+      }
+      // H_k dbar = H_{k-1} dbar + entry k-1's rank-2 term;  gbar_k, a_k, a_{k-1}
+      const float e1 = c * rho * sd - rho * wd, e2 = -rho * sd;
+      float tr[1] = {0.f};
+      const float* g0r = k == 1 ? Gr : nullptr;
+      for (int i = tid; i < Pv; i += kAdjBlock) {
+        const float ybar = p2[i] + hw[i];
+        const float hk = hd[i] + e1 * sv[i] + e2 * wv[i];
+        gk[i] = gbp[i] - hk + ybar;
+        gbp[i] = -ybar;
+        const float af = ak[i] + wb[i];
+        ak[i] = af;
+        Ar[(size_t)(k - 1) * Pv + i] = -wb[i];
+        tr[0] += af * gv[i];
+        if (k == 1 && i < P) tr[0] -= wb[i] * g0r[i];  // a_0 = -wbar_1
+      }
+      block_sum<1, kAdjWaves>(tr, scratch, buf);
+      buf ^= 1;
+      trace += tr[0];
+      if (k == 1) {
+        // gamma = clamp(q, min 1e-4), q = t / clamp(yy, min 1e-5); its adjoint is tr(H_0' adjoint)
+        const float yyc = clamp_min(yy, 1e-5f);
+        const float q = t / yyc;
+        const float qbar = q >= 1e-4f ? trace : 0.f;  // clamp backward passes where input >= min
+        const float tg = qbar / yyc;
+        const float yybar = yy >= 1e-5f ? -qbar * q / yyc : 0.f;
+        for (int i = tid; i < Pv; i += kAdjBlock) {
+          const float extra = tg * sv[i] + 2.0f * yybar * yv[i];
+          sbp[i] += tg * yv[i];
+          gk[i] += extra;
+          gbp[i] -= extra;
+        }
+      }
+    }
+    // ---- g_k = dE/dx(x_k): xbar += Hess E gbar_k, obsbar += (d2E/dobs dx) gbar_k ----
+    const float* xk = X + (size_t)k * Pv;
+    for (int i = tid; i < Pv; i += kAdjBlock) {
+      xd[i] = Dual(i < P ? xk[i] : 0.f, i < P ? gk[i] : 0.f);
+      gd[i] = Dual(0.f);
+    }
+    __syncthreads();
+    Dual E(0.f), unused(0.f);
+    ba_eval<true, false, false, false, false, RES, Dual, kAdjWaves>(L, xd, nullptr, 0.f, obs, vis, gd, views, vpart,
+                                                                   scratch, buf, E, unused, obsd);
+    for (int i = tid; i < P; i += kAdjBlock) xb[i] += gd[i].t;
+    for (int i = tid; i < 2 * MN; i += kAdjBlock) obsacc[i] += obsd[i].t;
+    __syncthreads();
+  }
+  for (int i = tid; i < P; i += kAdjBlock) a.x0_grad[(size_t)b * P + i] = xb[i];
+  if (a.obs_grad)
+    for (int i = tid; i < 2 * MN; i += kAdjBlock) a.obs_grad[(size_t)b * 2 * MN + i] = obsacc[i];
+}
+
+template <int RES>
+static void launch_adjoint(const AdjointArgs& a, int B, int lds, int gm, hipStream_t s) {
+  auto go = [&](auto kernel) {
+    if (lds > 64 * 1024)
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    hipLaunchKernelGGL(kernel, dim3(B), dim3(kAdjBlock), lds, s, a);
+  };
+  if (gm <= 1) go(bfgs_ba_adjoint_kernel<RES, 1>);
+  else if (gm == 2) go(bfgs_ba_adjoint_kernel<RES, 2>);
+  else if (gm == 3) go(bfgs_ba_adjoint_kernel<RES, 3>);
+  else go(bfgs_ba_adjoint_kernel<RES, 4>);
+}
+
+static int adjoint_check(const DavaScene* s, const DavaSolverConfig* c) {
+  if (!s || !c) return DAVA_ERR_INVALID_ARGUMENT;
+  if (s->batch < 0 || s->num_views < 2 || s->num_points < 1) return DAVA_ERR_INVALID_ARGUMENT;
+  const int P = 3 + 3 * s->num_points + 6 * (s->num_views - 1) + (s->distortion ? 5 : 0);
+  if (s->num_parameters != P) return DAVA_ERR_INVALID_ARGUMENT;
+  if (s->residual != DAVA_RESIDUAL_SQUARED_REPROJECTION && s->residual != DAVA_RESIDUAL_RAY_ANGLE)
+    return DAVA_ERR_INVALID_ARGUMENT;
+  if (s->residual == DAVA_RESIDUAL_RAY_ANGLE && s->distortion) return DAVA_ERR_UNSUPPORTED;
+  if (c->hessian_mode != DAVA_HESSIAN_COMPACT || c->iterations < 1 || P > 1024) return DAVA_ERR_UNSUPPORTED;
+  const TapeLayout tl = tape_layout(s->batch, P, c->iterations);
+  if (carve_adjoint(s->num_views, s->num_points, tl.Pv, tl.T).total_bytes > 160 * 1024) return DAVA_ERR_UNSUPPORTED;
+  return DAVA_OK;
+}
+
+}  // namespace dava
+
+using namespace dava;
+
+extern "C" size_t dava_ba_solve_backward_workspace_bytes(const DavaScene* scene, const DavaSolverConfig* config) {
+  if (adjoint_check(scene, config) != DAVA_OK) return 0;
+  const TapeLayout tl = tape_layout(scene->batch, scene->num_parameters, config->iterations);
+  return (size_t)scene->batch * tl.K * tl.Pv * sizeof(float) + 256;
+}
+
+extern "C" int dava_ba_solve_backward(const DavaScene* scene, const DavaSolverConfig* config, const void* tape,
+                                      size_t tape_bytes, const int32_t* status, const float* x_out_grad,
+                                      float* x0_grad, float* observations_grad, void* workspace,
+                                      size_t workspace_bytes, void* stream) {
+  const int st = adjoint_check(scene, config);
+  if (st != DAVA_OK) return st;
+  if (scene->batch == 0) return DAVA_OK;
+  if (!scene->observations || !scene->visibility || !tape || !status || !x_out_grad || !x0_grad)
+    return DAVA_ERR_INVALID_ARGUMENT;
+  const TapeLayout tl = tape_layout(scene->batch, scene->num_parameters, config->iterations);
+  if (tape_bytes < tl.queue_byte) return DAVA_ERR_WORKSPACE;
+  if (!workspace || workspace_bytes < (size_t)scene->batch * tl.K * tl.Pv * sizeof(float)) return DAVA_ERR_WORKSPACE;
+  AdjointArgs a;
+  a.L = Layout{scene->num_views, scene->num_points, scene->num_parameters, scene->distortion ? 1 : 0};
+  a.Pv = tl.Pv;
+  a.K = tl.K;
+  a.tl = tl;
+  a.tape = static_cast<const float*>(tape);
+  a.obs = scene->observations;
+  a.vis = scene->visibility;
+  a.status = status;
+  a.xbar = x_out_grad;
+  a.x0_grad = x0_grad;
+  a.obs_grad = observations_grad;
+  a.arows = static_cast<float*>(workspace);
+  const int lds = carve_adjoint(scene->num_views, scene->num_points, tl.Pv, tl.T).total_bytes;
+  const int gm = (tl.Pv / 4 + kWave - 1) / kWave;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (scene->residual == DAVA_RESIDUAL_RAY_ANGLE) launch_adjoint<DAVA_RESIDUAL_RAY_ANGLE>(a, scene->batch, lds, gm, s);
+  else launch_adjoint<DAVA_RESIDUAL_SQUARED_REPROJECTION>(a, scene->batch, lds, gm, s);
+  return hipGetLastError() == hipSuccess ? DAVA_OK : DAVA_ERR_LAUNCH;
+}

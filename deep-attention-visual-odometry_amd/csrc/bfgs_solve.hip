@@ -26,6 +26,7 @@
 #include <cstdlib>
 
 #include "ba_objective.hpp"
+#include "dava_tape.hpp"
 
 namespace dava {
 
@@ -46,6 +47,11 @@ struct SolveArgs {
   float* vecs;    // GV mode: B x kVectors x Pv floats (else unused)
   unsigned long long* phase_cycles;  // DAVA_PHASE_TIMING builds: B x kPhases (else null)
   int* queue;     // work-queue counter (zeroed before the launch), or null: problem = blockIdx.x
+  // recording solve (dava_ba_solve_record, dava_tape.hpp): x_k and g_k rows, (alpha, rho, c, gamma)
+  float* tape_x;  // (B, K, Pv) or null
+  float* tape_g;  // (B, K, Pv)
+  float* tape_s;  // (B, tape_T)
+  int tape_T;
 };
 
 struct LdsCarve {
@@ -771,6 +777,10 @@ __global__ __launch_bounds__(kWave * NW, DAVA_SOLVE_WAVES_PER_EU) void bfgs_ba_s
   #endif
     for (int k = 0; k < a.iters; ++k) {
       { float* t = g; g = gp; gp = t; }  // gp <- previous gradient; g <- (trial) gradient buffer
+      if (a.tape_x) {  // recording: x_k (the same threads wrote x[i] when the last step was taken)
+        float* r = a.tape_x + ((size_t)b * a.iters + k) * Pv;
+        for (int i = tid; i < Pv; i += BLOCK) r[i] = x[i];  // (pads are zero)
+      }
       if (have_next) {
         E = E_next;
       } else {
@@ -780,6 +790,10 @@ __global__ __launch_bounds__(kWave * NW, DAVA_SOLVE_WAVES_PER_EU) void bfgs_ba_s
         ++evals;
       }
       DAVA_PHASE(0);
+      if (a.tape_g) {  // recording: g_k
+        float* r = a.tape_g + ((size_t)b * a.iters + k) * Pv;
+        for (int i = tid; i < Pv; i += BLOCK) r[i] = g[i];
+      }
       if (!(E > a.thr)) { reason = DAVA_STOP_ERROR; break; }
 
       // phi'(0) = d . g is accumulated where d is formed (same per-thread order as a separate
@@ -805,6 +819,7 @@ __global__ __launch_bounds__(kWave * NW, DAVA_SOLVE_WAVES_PER_EU) void bfgs_ba_s
           block_sum<4, NW>(r, scratch, buf); buf ^= 1;
           const float gamma = clamp_min(r[0] / clamp_min(r[1], 1e-5f), 1e-4f);
           gamma0 = gamma;
+          if (a.tape_s && tid == 0) a.tape_s[(size_t)b * a.tape_T + 3 * a.iters] = gamma;
           rho = r[0] <= 0.f ? 0.f : 1.0f / r[0];
           c = 1.0f + rho * (gamma * r[1]);
           sg = r[2];
@@ -898,7 +913,14 @@ __global__ __launch_bounds__(kWave * NW, DAVA_SOLVE_WAVES_PER_EU) void bfgs_ba_s
             float* wr = WH + (size_t)(k - 1) * Pv;
             for (int i = tid; i < Pv; i += BLOCK) { sr[i] = s_cur[i]; wr[i] = hy_new[i]; }
           }
-          if (tid == 0) { hrho[k - 1] = rho; hc[k - 1] = c; }
+          if (tid == 0) {
+            hrho[k - 1] = rho;
+            hc[k - 1] = c;
+            if (a.tape_s) {
+              a.tape_s[(size_t)b * a.tape_T + a.iters + k - 1] = rho;
+              a.tape_s[(size_t)b * a.tape_T + 2 * a.iters + k - 1] = c;
+            }
+          }
         }
       }
 
@@ -977,6 +999,7 @@ __global__ __launch_bounds__(kWave * NW, DAVA_SOLVE_WAVES_PER_EU) void bfgs_ba_s
         if (a_lo == a_hi) zoom = false;
       }
       const float alpha = a_hi;
+      if (a.tape_s && tid == 0) a.tape_s[(size_t)b * a.tape_T + k] = alpha;
       have_next = evaluated && last_al == alpha;
       E_next = last_fa;
       if (have_next && last_same) {  // x_{k+1} == x_k bitwise: its gradient is g itself
@@ -1280,14 +1303,23 @@ static void launch_solve(const SolveArgs& a, int B, int lds, hipStream_t s, int 
   else launch_solve_res<MODE, GV, DAVA_RESIDUAL_SQUARED_REPROJECTION, XL>(a, B, lds, s, nw);
 }
 
-extern "C" int dava_ba_solve(const DavaScene* scene, const DavaSolverConfig* config, const float* x0,
-                             float* x_out, float* error_out, int32_t* status_out, void* workspace,
-                             size_t workspace_bytes, void* stream) {
+// A recording solve (the tape of dava_tape.hpp) needs COMPACT mode with the O(P) state in LDS and
+// rows of at most 4 x 64 float4 groups (P <= 1024), the shapes the adjoint kernel implements.
+static bool tape_supported(const DavaScene* scene, const DavaSolverConfig* config) {
+  if (config->hessian_mode != DAVA_HESSIAN_COMPACT || config->iterations < 1) return false;
+  const int kcap = compact_capacity(config);
+  return kcap <= kMaxCompactEntries && !use_gv(scene, kcap) && scene->num_parameters <= 1024;
+}
+
+static int solve_impl(const DavaScene* scene, const DavaSolverConfig* config, const float* x0, float* x_out,
+                      float* error_out, int32_t* status_out, void* workspace, size_t workspace_bytes, bool record,
+                      void* stream) {
   int st = check_scene(scene);
   if (st != DAVA_OK) return st;
   if (!config || config->iterations < 0 || config->max_line_search_trials < 0) return DAVA_ERR_INVALID_ARGUMENT;
   const int mode = config->hessian_mode;
   if (mode != DAVA_HESSIAN_DENSE && mode != DAVA_HESSIAN_COMPACT) return DAVA_ERR_INVALID_ARGUMENT;
+  if (record && !tape_supported(scene, config)) return DAVA_ERR_UNSUPPORTED;
   if (scene->batch == 0) return DAVA_OK;
   if (!x0 || !x_out) return DAVA_ERR_INVALID_ARGUMENT;
   const int kcap = mode == DAVA_HESSIAN_COMPACT ? compact_capacity(config) : 0;
@@ -1295,12 +1327,14 @@ extern "C" int dava_ba_solve(const DavaScene* scene, const DavaSolverConfig* con
   const bool gv = use_gv(scene, kcap);
   const bool xl = use_xl(scene, kcap, gv);
   const int nw = solve_waves_for(scene, gv, mode);
-  const int lcap = mode == DAVA_HESSIAN_COMPACT ? lds_history_entries(scene, kcap, gv, nw) : 0;
+  // recording keeps every history entry in HBM (the adjoint reads them back; bitwise the same run)
+  const int lcap = mode == DAVA_HESSIAN_COMPACT && !record ? lds_history_entries(scene, kcap, gv, nw) : 0;
   const int lds = lds_bytes_for(scene, kcap, gv, lcap, xl, nw);
   if (lds > kMaxLds) return DAVA_ERR_UNSUPPORTED;
   const size_t vec = gv ? gv_vector_bytes(scene) : 0;
-  const size_t need = solve_state_bytes(scene, config);
-  const bool uses_ws = gv || (mode == DAVA_HESSIAN_DENSE ? config->iterations > 2 : config->iterations > 1);
+  const TapeLayout tl = tape_layout(scene->batch, scene->num_parameters, config->iterations);
+  const size_t need = record ? tl.queue_byte : solve_state_bytes(scene, config);
+  const bool uses_ws = record || gv || (mode == DAVA_HESSIAN_DENSE ? config->iterations > 2 : config->iterations > 1);
   if (uses_ws && (!workspace || workspace_bytes < need)) return DAVA_ERR_WORKSPACE;
   // the work queue needs its counter in the workspace's tail (dava_ba_solve_workspace_bytes
   // includes it); a workspace sized without it runs one workgroup per problem instead
@@ -1330,6 +1364,15 @@ extern "C" int dava_ba_solve(const DavaScene* scene, const DavaSolverConfig* con
   a.lcap = lcap;
   a.phase_cycles = nullptr;
   a.queue = queue ? reinterpret_cast<int*>(static_cast<char*>(workspace) + need) : nullptr;
+  a.tape_x = a.tape_g = a.tape_s = nullptr;
+  a.tape_T = tl.T;
+  if (record) {
+    float* t = static_cast<float*>(workspace);
+    a.hess = t + tl.hist;
+    a.tape_x = t + tl.x;
+    a.tape_g = t + tl.g;
+    a.tape_s = t + tl.scal;
+  }
   hipStream_t s = static_cast<hipStream_t>(stream);
   if (queue && hipMemsetAsync(a.queue, 0, sizeof(int), s) != hipSuccess) return DAVA_ERR_LAUNCH;
 #if DAVA_PHASE_TIMING
@@ -1376,6 +1419,24 @@ extern "C" int dava_ba_solve(const DavaScene* scene, const DavaSolverConfig* con
   }
 #endif
   return launched ? DAVA_OK : DAVA_ERR_LAUNCH;
+}
+
+extern "C" int dava_ba_solve(const DavaScene* scene, const DavaSolverConfig* config, const float* x0,
+                             float* x_out, float* error_out, int32_t* status_out, void* workspace,
+                             size_t workspace_bytes, void* stream) {
+  return solve_impl(scene, config, x0, x_out, error_out, status_out, workspace, workspace_bytes, false, stream);
+}
+
+extern "C" size_t dava_ba_solve_tape_bytes(const DavaScene* scene, const DavaSolverConfig* config) {
+  if (check_scene(scene, false) != DAVA_OK || !config || !tape_supported(scene, config)) return 0;
+  return tape_layout(scene->batch, scene->num_parameters, config->iterations).total_bytes;
+}
+
+extern "C" int dava_ba_solve_record(const DavaScene* scene, const DavaSolverConfig* config, const float* x0,
+                                    float* x_out, float* error_out, int32_t* status_out, void* tape,
+                                    size_t tape_bytes, void* stream) {
+  if (!status_out && scene && scene->batch > 0) return DAVA_ERR_INVALID_ARGUMENT;  // the adjoint needs the steps
+  return solve_impl(scene, config, x0, x_out, error_out, status_out, tape, tape_bytes, true, stream);
 }
 
 template <bool G, bool S, bool T, bool GV, int RES>

@@ -73,6 +73,13 @@ SIGNATURES = {
                                      _vp, ctypes.c_size_t, _vp]),
     "dava_ba_evaluate": (ctypes.c_int, [ctypes.POINTER(DavaScene), _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "dava_ba_second_order": (ctypes.c_int, [ctypes.POINTER(DavaScene)] + [_vp] * 8),
+    "dava_ba_solve_tape_bytes": (ctypes.c_size_t, [ctypes.POINTER(DavaScene), ctypes.POINTER(DavaSolverConfig)]),
+    "dava_ba_solve_record": (ctypes.c_int, [ctypes.POINTER(DavaScene), ctypes.POINTER(DavaSolverConfig), _vp, _vp,
+                                            _vp, _vp, _vp, ctypes.c_size_t, _vp]),
+    "dava_ba_solve_backward_workspace_bytes": (ctypes.c_size_t, [ctypes.POINTER(DavaScene),
+                                                                 ctypes.POINTER(DavaSolverConfig)]),
+    "dava_ba_solve_backward": (ctypes.c_int, [ctypes.POINTER(DavaScene), ctypes.POINTER(DavaSolverConfig), _vp,
+                                              ctypes.c_size_t, _vp, _vp, _vp, _vp, _vp, ctypes.c_size_t, _vp]),
     "dava_abi_version": (ctypes.c_int, []),
     "dava_status_string": (ctypes.c_char_p, [ctypes.c_int]),
     "dava_device_arch": (ctypes.c_char_p, []),

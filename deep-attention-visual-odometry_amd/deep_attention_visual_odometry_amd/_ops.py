@@ -182,6 +182,73 @@ def _(x, observations, visibility, num_views, num_points, distortion, direction,
             torch.empty_like(observations) if (want_obs and want_hv) else x.new_empty((0,)))
 
 
+@torch.library.custom_op("dava::ba_solve_record", mutates_args=(), device_types=_CUDA)
+def ba_solve_record(x0: Tensor, observations: Tensor, visibility: Tensor, num_views: int, num_points: int,
+                    distortion: bool, sufficient_decrease: float, curvature: float, error_threshold: float,
+                    iterations: int, minimum_step: float, max_line_search_trials: int, strong: bool,
+                    residual: int) -> Tuple[Tensor, Tensor, Tensor]:
+    """``dava_ba_solve_record``: the fused COMPACT solve (bitwise ``ba_solve``'s x and status) plus the
+    tape the adjoint replays.  Returns (x, status (B, 4) int32, tape uint8)."""
+    lib = N.load_library()
+    _check_scene_tensors(x0, observations, visibility, num_views, num_points, distortion)
+    b, dev = x0.shape[0], x0.device
+    sc = scene_struct(observations, visibility, num_views, num_points, distortion, b, residual)
+    cfg = solver_config(sufficient_decrease, curvature, error_threshold, iterations, minimum_step,
+                        max_line_search_trials, strong, N.DAVA_HESSIAN_COMPACT)
+    need = int(lib.dava_ba_solve_tape_bytes(sc, cfg))
+    if need == 0:
+        raise ValueError("this scene / configuration has no fused adjoint (compact mode, P <= 1024, "
+                         "iterations >= 1, the O(P) state in LDS)")
+    tape = torch.empty(need, dtype=torch.uint8, device=dev)
+    x_out = torch.empty_like(x0)
+    status = torch.empty((b, N.STATUS_WORDS), device=dev, dtype=torch.int32)
+    with torch.cuda.device(dev):
+        N.check(lib.dava_ba_solve_record(sc, cfg, N.ptr(x0), N.ptr(x_out), None, N.ptr(status), N.ptr(tape),
+                                         tape.numel(), N.stream_of(dev)), "dava_ba_solve_record")
+    return x_out, status, tape
+
+
+@ba_solve_record.register_fake
+def _(x0, observations, visibility, num_views, num_points, distortion, sufficient_decrease, curvature,
+      error_threshold, iterations, minimum_step, max_line_search_trials, strong, residual):
+    b = x0.shape[0]
+    ctx = torch.library.get_ctx()
+    return (torch.empty_like(x0), x0.new_empty((b, N.STATUS_WORDS), dtype=torch.int32),
+            x0.new_empty((ctx.new_dynamic_size(),), dtype=torch.uint8))
+
+
+@torch.library.custom_op("dava::ba_solve_backward", mutates_args=(), device_types=_CUDA)
+def ba_solve_backward(x_out_grad: Tensor, tape: Tensor, status: Tensor, observations: Tensor, visibility: Tensor,
+                      num_views: int, num_points: int, distortion: bool, iterations: int, residual: int,
+                      want_observations: bool) -> Tuple[Tensor, Tensor]:
+    """``dava_ba_solve_backward``: (dL/dx0, dL/dobs or empty) of a recorded solve for dL/dx_out."""
+    lib = N.load_library()
+    _check_scene_tensors(x_out_grad, observations, visibility, num_views, num_points, distortion)
+    b, dev = x_out_grad.shape[0], x_out_grad.device
+    if tuple(status.shape) != (b, N.STATUS_WORDS) or status.dtype != torch.int32 or not status.is_contiguous():
+        raise ValueError("status must be the recording call's contiguous (B, 4) int32 tensor")
+    sc = scene_struct(observations, visibility, num_views, num_points, distortion, b, residual)
+    cfg = solver_config(1e-4, 0.9, 1e-4, iterations, 1e-8, 1000, True, N.DAVA_HESSIAN_COMPACT)
+    need = int(lib.dava_ba_solve_backward_workspace_bytes(sc, cfg))
+    if need == 0:
+        raise ValueError("this scene / configuration has no fused adjoint")
+    ws = torch.empty(need, dtype=torch.uint8, device=dev)
+    gx = torch.empty_like(x_out_grad)
+    gobs = torch.empty_like(observations) if want_observations else _empty0(x_out_grad)
+    with torch.cuda.device(dev):
+        N.check(lib.dava_ba_solve_backward(sc, cfg, N.ptr(tape), tape.numel(), N.ptr(status), N.ptr(x_out_grad),
+                                           N.ptr(gx), N.ptr(gobs) if want_observations else None, N.ptr(ws),
+                                           ws.numel(), N.stream_of(dev)), "dava_ba_solve_backward")
+    return gx, gobs
+
+
+@ba_solve_backward.register_fake
+def _(x_out_grad, tape, status, observations, visibility, num_views, num_points, distortion, iterations, residual,
+      want_observations):
+    return (torch.empty_like(x_out_grad),
+            torch.empty_like(observations) if want_observations else x_out_grad.new_empty((0,)))
+
+
 # ------------------------------------------------- generic BFGS building blocks
 
 def _square_batch(h: Tensor) -> Tuple[int, int]:
@@ -449,7 +516,7 @@ def _(focal, cx, cy, translation, lie, world, target, visibility, minimum_z_dist
             focal.new_empty((b, e, 3 + 6 * m + 3 * n - 7) if want_gradient else (0,)))
 
 
-OPS = ("ba_solve", "ba_evaluate", "ba_second_order", "bfgs_update_inverse_hessian",
+OPS = ("ba_solve", "ba_solve_record", "ba_solve_backward", "ba_evaluate", "ba_second_order", "bfgs_update_inverse_hessian",
        "bfgs_update_inverse_hessian_backward", "bfgs_initial_scale", "bfgs_initial_scale_backward",
        "bfgs_scale_matrix", "bfgs_scale_matrix_backward", "bfgs_search_direction", "bfgs_search_direction_backward",
        "wolfe_init", "wolfe_propose", "wolfe_update", "l1_camera_evaluate")

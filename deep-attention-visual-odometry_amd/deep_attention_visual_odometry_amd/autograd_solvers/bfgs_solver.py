@@ -26,6 +26,7 @@ cross term, csrc/ba_second_order.hip), so gradients reach captured observations.
 
 Not supported (raises rather than silently falling back): CPU tensors.
 """
+import os
 from typing import Callable, Optional
 
 import torch
@@ -89,9 +90,36 @@ class BFGSSolver(Module):
         else:
             error_threshold, num_iterations = self.error_threshold, self.iterations
         stochastic = self.training and (self.drop_path_p > 0.0 or self.return_second_last)
-        if isinstance(error_function, ReprojectionError) and not stochastic and not parameters.requires_grad:
-            return self._fused(parameters, error_function, error_threshold, num_iterations)
+        if isinstance(error_function, ReprojectionError) and not stochastic:
+            if not parameters.requires_grad:
+                return self._fused(parameters, error_function, error_threshold, num_iterations)
+            if self._adjoint_available(parameters, error_function, num_iterations):
+                return self._fused_differentiable(parameters, error_function, error_threshold, num_iterations)
         return self._generic(parameters, error_function, error_threshold, num_iterations)
+
+    def _adjoint_available(self, parameters, fn: ReprojectionError, num_iterations) -> bool:
+        """Differentiating through a fused objective's solve runs the recording solve + adjoint
+        kernel (compact history; C1-C3 shapes) unless dense mode was asked for or
+        DAVA_GENERIC_BACKWARD is set (then: the generic loop, graph kept by torch)."""
+        if self.hessian_mode == "dense" or os.environ.get("DAVA_GENERIC_BACKWARD"):
+            return False
+        if parameters.dtype != torch.float32 or num_iterations < 1 or num_iterations > self.MAX_COMPACT_ENTRIES + 1:
+            return False
+        return native_ops.solve_tape_supported(max(parameters.numel() // parameters.size(-1), 1), fn.num_views,
+                                               fn.num_points, fn.distortion, num_iterations, fn.residual)
+
+    def _fused_differentiable(self, parameters, fn: ReprojectionError, error_threshold, num_iterations):
+        lead = parameters.shape[:-1]
+        if fn.batch_shape != lead:
+            raise ValueError(f"ReprojectionError batch shape {tuple(fn.batch_shape)} != parameters {tuple(lead)}")
+        x0 = parameters.reshape(-1, parameters.size(-1))
+        x, status = native_ops.ba_solve_differentiable(
+            x0, fn.observations.reshape(-1, fn.num_views, fn.num_points, 2),
+            fn.visibility.reshape(-1, fn.num_views, fn.num_points), fn.num_views, fn.num_points, fn.distortion,
+            sufficient_decrease=self.sufficient_decrease, curvature=self.curvature, error_threshold=error_threshold,
+            iterations=num_iterations, minimum_step=self.minimum_step, residual=fn.residual)
+        self.last_status = status
+        return x.reshape(parameters.shape)
 
     def _fused(self, parameters, fn: ReprojectionError, error_threshold, num_iterations):
         lead = parameters.shape[:-1]

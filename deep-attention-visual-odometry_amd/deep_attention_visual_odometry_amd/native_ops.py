@@ -83,6 +83,58 @@ def ba_solve(x0: torch.Tensor, observations: torch.Tensor, visibility: torch.Ten
     return x, (err if want_error else None), (status if want_status else None)
 
 
+def solve_tape_supported(batch: int, num_views: int, num_points: int, distortion: bool, iterations: int,
+                         residual: int = N.DAVA_RESIDUAL_SQUARED_REPROJECTION) -> bool:
+    """Host-only: does this shape have the fused adjoint (``dava_ba_solve_tape_bytes`` > 0)?"""
+    lib = N.load_library()
+    sc = scene_struct(None, None, num_views, num_points, distortion, max(int(batch), 1), residual)
+    cfg = solver_config(1e-4, 0.9, 1e-4, iterations, 1e-8, 1000, True, N.DAVA_HESSIAN_COMPACT)
+    return int(lib.dava_ba_solve_tape_bytes(sc, cfg)) > 0
+
+
+class _FusedSolve(torch.autograd.Function):
+    """x_out = solve(x0, obs) in one recording launch; its backward is the adjoint kernel
+    (csrc/bfgs_adjoint.hip), which replays the tape: the reference's create_graph gradient
+    through BFGSSolver.forward (bfgs_solver.py:85, :133-135, :213-215) without a (B, P, P)
+    inverse Hessian per iteration.  Not differentiable twice."""
+
+    @staticmethod
+    def forward(ctx, x0, observations, visibility, num_views, num_points, distortion, residual, cfg):
+        c1, c2, thr, iters, min_step, trials, strong = cfg
+        x0c = _fp32_on_device(x0, "parameters")
+        obs, vis = _scene_inputs(x0c, observations, visibility)
+        x, status, tape = torch.ops.dava.ba_solve_record(
+            x0c, obs, vis, int(num_views), int(num_points), bool(distortion), float(c1), float(c2), float(thr),
+            int(iters), float(min_step), int(trials), bool(strong), int(residual))
+        ctx.save_for_backward(tape, status, obs, vis)
+        ctx.meta = (int(num_views), int(num_points), bool(distortion), int(iters), int(residual))
+        ctx.mark_non_differentiable(status)
+        return x, status
+
+    @staticmethod
+    @torch.autograd.function.once_differentiable
+    def backward(ctx, x_grad, _status_grad):
+        tape, status, obs, vis = ctx.saved_tensors
+        m, n, dist, iters, residual = ctx.meta
+        need_x, need_obs = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
+        if x_grad is None:
+            return (None,) * 8
+        gx, gobs = torch.ops.dava.ba_solve_backward(_c(x_grad.to(torch.float32)), tape, status, obs, vis, m, n, dist,
+                                                    iters, residual, bool(need_obs))
+        return (gx if need_x else None, gobs if need_obs else None, None, None, None, None, None, None)
+
+
+def ba_solve_differentiable(x0: torch.Tensor, observations: torch.Tensor, visibility: torch.Tensor, num_views: int,
+                            num_points: int, distortion: bool, *, sufficient_decrease: float = 1e-4,
+                            curvature: float = 0.9, error_threshold: float = 1e-4, iterations: int = 1000,
+                            minimum_step: float = 1e-8, max_line_search_trials: int = 1000, strong: bool = True,
+                            residual: int = N.DAVA_RESIDUAL_SQUARED_REPROJECTION):
+    """The fused COMPACT solve as an autograd node w.r.t. x0 and the observations.
+    Returns (x, status)."""
+    cfg = (sufficient_decrease, curvature, error_threshold, iterations, minimum_step, max_line_search_trials, strong)
+    return _FusedSolve.apply(x0, observations, visibility, num_views, num_points, distortion, residual, cfg)
+
+
 def solve_workspace_bytes(batch: int, num_views: int, num_points: int, distortion: bool,
                           hessian_mode: int = N.DAVA_HESSIAN_DENSE, iterations: int = 1000) -> int:
     lib = N.load_library()

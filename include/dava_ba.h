@@ -131,6 +131,33 @@ int dava_ba_solve(const DavaScene* scene, const DavaSolverConfig* config, const 
                   float* error_out, int32_t* status_out, void* workspace, size_t workspace_bytes,
                   void* stream);
 
+/* ---- differentiating THROUGH the fused solve (the reference's create_graph mode,
+ * bfgs_solver.py:85, :133-135, :213-215: every iteration's gradient kept in the graph, the
+ * line search's step size a constant) without a dense (B, P, P) inverse Hessian per iteration.
+ * A recording solve keeps a tape in HBM (x_k, g_k, the compact history rows, step sizes; see
+ * csrc/dava_tape.hpp); the adjoint replays it backwards, one workgroup per problem.
+ * COMPACT mode, P <= 1024 with the O(P) state in LDS (C1-C3 shapes); otherwise the size
+ * queries return 0 and the calls DAVA_ERR_UNSUPPORTED. */
+
+/* Bytes of the tape (including the work-queue counter's 256 bytes), or 0 if unsupported. */
+size_t dava_ba_solve_tape_bytes(const DavaScene* scene, const DavaSolverConfig* config);
+
+/* dava_ba_solve (bitwise the same x_out, error_out and status_out) that also writes the tape.
+ * status_out is required (the adjoint reads the steps each problem took). */
+int dava_ba_solve_record(const DavaScene* scene, const DavaSolverConfig* config, const float* x0, float* x_out,
+                         float* error_out, int32_t* status_out, void* tape, size_t tape_bytes, void* stream);
+
+/* Device workspace of dava_ba_solve_backward, or 0 if unsupported. */
+size_t dava_ba_solve_backward_workspace_bytes(const DavaScene* scene, const DavaSolverConfig* config);
+
+/* Vector-Jacobian product of the recorded solve: given x_out_grad = dL/dx_out (B, P), writes
+ *   x0_grad            (B, P)        dL/dx0
+ *   observations_grad  (B, M, N, 2)  dL/dobs (or NULL)
+ * scene/config/status must be those of the recording call, the tape unmodified. */
+int dava_ba_solve_backward(const DavaScene* scene, const DavaSolverConfig* config, const void* tape,
+                           size_t tape_bytes, const int32_t* status, const float* x_out_grad, float* x0_grad,
+                           float* observations_grad, void* workspace, size_t workspace_bytes, void* stream);
+
 /* One objective evaluation per problem at x + alpha[b] * direction.
  * Replaces one call of the reference-composed error function plus
  * torch.autograd.grad (bfgs_solver.py:131-135 / wolfe_conditions.py:134-143):
