@@ -447,6 +447,129 @@ __device__ __forceinline__ void compact_products_wide(int P, int Pv, int nh, con
   }
 }
 
+// GV mode, COMPACT, iteration k >= 2: the workgroup-wide history pass of compact_products_wide and
+// everything up to the line search in ONE sweep over this thread's float4 column groups, from
+// registers: H'y and H'g stay in registers (never written to the workspace), s_{k-1} is loaded
+// once, the four curvature dots go through one block reduction, then d = -H_k g (same per-element
+// formula as the generic tail), phi'(0)'s partial d.g, and the history append (W row <- H'y,
+// S row <- s) -- instead of four more passes over workspace vectors (C5: the direction phase was
+// 9% of the solve, profiles/r02_phase_cycles_c5.log).  Returns this thread's d.g partial.
+#ifndef DAVA_GV_FUSED_TAIL
+#define DAVA_GV_FUSED_TAIL 1
+#endif
+template <int GT, int NW>
+__device__ __forceinline__ float wide_direction(int P, int Pv, int nh, const float* __restrict__ S,
+                                                const float* __restrict__ W, float* hrho, float* hc, float gamma0,
+                                                const float* g, const float* gp, const float* s_cur, float* d,
+                                                float* s_row, float* w_row, float* scratch, int& buf, int entry,
+                                                float* tape_rho, float* tape_c) {
+  constexpr int BLOCK = kWave * NW;
+  constexpr int E = GT <= 2 ? 2 : 1;
+  const int tid = threadIdx.x;
+  const int G = (P + 3) / 4;
+  const f4v z = f4v{0, 0, 0, 0};
+  f4v y[GT], gg[GT], pa[GT], pb[GT];
+#pragma unroll
+  for (int u = 0; u < GT; ++u) {
+    const int q = tid + u * BLOCK;
+    y[u] = gg[u] = pa[u] = pb[u] = z;
+    if (q < G) {
+      gg[u] = *reinterpret_cast<const f4v*>(g + 4 * q);
+      y[u] = gg[u] - *reinterpret_cast<const f4v*>(gp + 4 * q);
+    }
+  }
+  auto dot4 = [](f4v a, f4v b) { const f4v t = a * b; return (t[0] + t[1]) + (t[2] + t[3]); };
+  for (int j = 0; j < nh; j += E) {
+    const int ne = min(E, nh - j);  // uniform
+    f4v s4[E][GT], w4[E][GT];
+    float dd[4 * E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+#pragma unroll
+      for (int u = 0; u < GT; ++u) {
+        const int q = tid + u * BLOCK;
+        s4[e][u] = w4[e][u] = z;
+        if (e < ne && q < G) {
+          s4[e][u] = *reinterpret_cast<const f4v*>(S + (size_t)(j + e) * Pv + 4 * q);
+          w4[e][u] = *reinterpret_cast<const f4v*>(W + (size_t)(j + e) * Pv + 4 * q);
+        }
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      dd[4 * e] = dd[4 * e + 1] = dd[4 * e + 2] = dd[4 * e + 3] = 0.0f;
+#pragma unroll
+      for (int u = 0; u < GT; ++u) {
+        dd[4 * e] += dot4(s4[e][u], y[u]);
+        dd[4 * e + 1] += dot4(w4[e][u], y[u]);
+        dd[4 * e + 2] += dot4(s4[e][u], gg[u]);
+        dd[4 * e + 3] += dot4(w4[e][u], gg[u]);
+      }
+    }
+    block_sum<4 * E, NW>(dd, scratch, buf);
+    buf ^= 1;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      if (e < ne) {
+        const float rho = hrho[j + e], cr = hc[j + e] * rho;
+        const float ay = cr * dd[4 * e] - rho * dd[4 * e + 1], by = -rho * dd[4 * e];
+        const float ag = cr * dd[4 * e + 2] - rho * dd[4 * e + 3], bg = -rho * dd[4 * e + 2];
+#pragma unroll
+        for (int u = 0; u < GT; ++u) {
+          pa[u] += ay * s4[e][u] + by * w4[e][u];
+          pb[u] += ag * s4[e][u] + bg * w4[e][u];
+        }
+      }
+    }
+  }
+  // H'y, H'g in registers; s_{k-1}; the curvature dots (s.y, H'y.y, s.g, H'y.g)
+  f4v sv[GT];
+  float r[4] = {0, 0, 0, 0};
+#pragma unroll
+  for (int u = 0; u < GT; ++u) {
+    const int q = tid + u * BLOCK;
+    pa[u] += gamma0 * y[u];
+    pb[u] += gamma0 * gg[u];
+    sv[u] = q < G ? *reinterpret_cast<const f4v*>(s_cur + 4 * q) : z;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      r[0] += sv[u][e] * y[u][e]; r[1] += pa[u][e] * y[u][e];
+      r[2] += sv[u][e] * gg[u][e]; r[3] += pa[u][e] * gg[u][e];
+    }
+  }
+  block_sum<4, NW>(r, scratch, buf);
+  buf ^= 1;
+  const float rho = r[0] <= 0.f ? 0.f : 1.0f / r[0];  // inverse_curvature (func_inverse_curvature.py:24-28)
+  const float c = 1.0f + rho * r[1];
+  const float sg = r[2], hyg = r[3];
+  const float rsg = rho * sg;
+  float dg = 0.f;
+#pragma unroll
+  for (int u = 0; u < GT; ++u) {
+    const int q = tid + u * BLOCK;
+    if (q < G) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int i = 4 * q + e;
+        if (i < P) {
+          const float sri = sv[u][e] * rho;
+          const float di = -1.0f * (pb[u][e] + sri * (c * sg) - sri * hyg - pa[u][e] * rsg);
+          d[i] = di;
+          dg += di * gg[u][e];
+        }
+      }
+      *reinterpret_cast<f4v*>(s_row + 4 * q) = sv[u];  // history entry `entry` = (s, H'y, rho, c)
+      *reinterpret_cast<f4v*>(w_row + 4 * q) = pa[u];
+    }
+  }
+  if (tid == 0) {
+    hrho[entry] = rho;
+    hc[entry] = c;
+    if (tape_rho) { *tape_rho = rho; *tape_c = c; }
+  }
+  return dg;
+}
+
 // COMPACT mode, single pass (P <= 1024, i.e. at most GM <= 4 float4 groups per lane):
 // the coefficients of entry j depend only on entry j's own dots, so one wave
 // loads the two rows of an entry into registers, reduces its 4 dots in-wave
@@ -808,8 +931,9 @@ __global__ __launch_bounds__(kWave * NW, DAVA_SOLVE_WAVES_PER_EU) void bfgs_ba_s
         }
       } else {
         float r[4] = {0, 0, 0, 0};
-        float rho, c, sg, hyg;
+        float rho = 0.f, c = 1.f, sg = 0.f, hyg = 0.f;
         bool deferred = false;  // the fused pass left its last cross-wave add to the pass below
+        bool tail_done = false;  // GV: wide_direction formed d and appended the history entry itself
         if (k == 1) {
           // H_0 = gamma I, gamma from N&W eq. 6.20 (bfgs_solver.py:159-167, 217-233)
           for (int i = tid; i < P; i += BLOCK) {
@@ -845,7 +969,21 @@ __global__ __launch_bounds__(kWave * NW, DAVA_SOLVE_WAVES_PER_EU) void bfgs_ba_s
             if constexpr (GV) {  // workgroup-wide single pass, else two passes
               const int GT = (G4 + kWave * NW - 1) / (kWave * NW);
               const int nh = k - 1;
-              if (!wide_history_pass(Pv, a.kcap, GV))
+              float* tr = a.tape_s ? a.tape_s + (size_t)b * a.tape_T + a.iters + k - 1 : nullptr;
+              float* tcp = tr ? tr + a.iters : nullptr;
+              float* srow = SH + (size_t)(k - 1) * Pv;
+              float* wrow = WH + (size_t)(k - 1) * Pv;
+              const bool fuse = DAVA_GV_FUSED_TAIL && wide_history_pass(Pv, a.kcap, GV) && k - 1 < a.kcap;
+              if (fuse) {
+                tail_done = true;
+                if (GT <= 1) dg = wide_direction<1, NW>(P, Pv, nh, SH, WH, hrho, hc, gamma0, g, gp, s_cur, d, srow, wrow, scratch, buf, k - 1, tr, tcp);
+                else if (GT == 2) dg = wide_direction<2, NW>(P, Pv, nh, SH, WH, hrho, hc, gamma0, g, gp, s_cur, d, srow, wrow, scratch, buf, k - 1, tr, tcp);
+                else if (GT == 3) dg = wide_direction<3, NW>(P, Pv, nh, SH, WH, hrho, hc, gamma0, g, gp, s_cur, d, srow, wrow, scratch, buf, k - 1, tr, tcp);
+                else if (GT == 4) dg = wide_direction<4, NW>(P, Pv, nh, SH, WH, hrho, hc, gamma0, g, gp, s_cur, d, srow, wrow, scratch, buf, k - 1, tr, tcp);
+                else if (GT == 5) dg = wide_direction<5, NW>(P, Pv, nh, SH, WH, hrho, hc, gamma0, g, gp, s_cur, d, srow, wrow, scratch, buf, k - 1, tr, tcp);
+                else if (GT == 6) dg = wide_direction<6, NW>(P, Pv, nh, SH, WH, hrho, hc, gamma0, g, gp, s_cur, d, srow, wrow, scratch, buf, k - 1, tr, tcp);
+                else dg = wide_direction<7, NW>(P, Pv, nh, SH, WH, hrho, hc, gamma0, g, gp, s_cur, d, srow, wrow, scratch, buf, k - 1, tr, tcp);
+              } else if (!wide_history_pass(Pv, a.kcap, GV))
                 compact_products<GV ? 8 : 1, NW>(P, Pv, nh, SH, WH, hcoef, hrho, hc, gamma0, g, gp, hy_new, hg);
               else if (GT <= 1) compact_products_wide<1, NW>(P, Pv, nh, SH, WH, hrho, hc, gamma0, g, gp, hy_new, hg, scratch, buf);
               else if (GT == 2) compact_products_wide<2, NW>(P, Pv, nh, SH, WH, hrho, hc, gamma0, g, gp, hy_new, hg, scratch, buf);
@@ -866,6 +1004,7 @@ __global__ __launch_bounds__(kWave * NW, DAVA_SOLVE_WAVES_PER_EU) void bfgs_ba_s
             compact_products<GV ? 8 : 1, NW>(P, Pv, k - 1, SH, WH, hcoef, hrho, hc, gamma0, g, gp, hy_new, hg);
           }
   #endif
+          if (!tail_done) {
           __syncthreads();
           DAVA_PHASE(1);
           if (deferred) {  // finish the fused pass's cross-wave sum here, all threads at once
@@ -888,9 +1027,11 @@ __global__ __launch_bounds__(kWave * NW, DAVA_SOLVE_WAVES_PER_EU) void bfgs_ba_s
           c = 1.0f + rho * r[1];
           sg = r[2];
           hyg = r[3];
+          }
         }
         // d = -H_k g,  H_k = H' + c (rho s) s^T - (rho s) (H'y)^T - (H'y) (rho s)^T
         const float rsg = rho * sg;
+        if (!tail_done)
         for (int i = tid; i < P; i += BLOCK) {
           const float sri = s_cur[i] * rho;
           const float di = -1.0f * (hg[i] + sri * (c * sg) - sri * hyg - hy_new[i] * rsg);
@@ -903,7 +1044,7 @@ __global__ __launch_bounds__(kWave * NW, DAVA_SOLVE_WAVES_PER_EU) void bfgs_ba_s
           { float* t = hy_pend; hy_pend = hy_new; hy_new = t; }
           pend_rho = rho;
           pend_c = c;
-        } else if (k - 1 < a.kcap) {
+        } else if (k - 1 < a.kcap && !tail_done) {
           // append U_k = (s, H y, rho, c) to the history (entry k-1), on-chip if it is one of the first lcap
           if (k - 1 < lcap) {
             float* sr = LH + (size_t)2 * (k - 1) * Pv;
