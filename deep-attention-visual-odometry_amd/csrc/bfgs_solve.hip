@@ -52,6 +52,7 @@ struct SolveArgs {
   float* tape_g;  // (B, K, Pv)
   float* tape_s;  // (B, tape_T)
   int tape_T;
+  int stagger;    // shader cycles the odd workgroups wait before starting (0: none)
 };
 
 struct LdsCarve {
@@ -817,6 +818,18 @@ __global__ __launch_bounds__(kWave * NW, DAVA_SOLVE_WAVES_PER_EU) void bfgs_ba_s
   // each takes the next problem when it finishes one, so a problem that stops early or runs a
   // long line search never leaves its slot idle.  Without a queue: problem = blockIdx.x.
   __shared__ int queued_problem;
+  // Staggered start (a.stagger > 0: every problem of the launch is resident at once): the odd
+  // workgroups -- dealt round-robin, so the odd XCDs -- start a.stagger shader cycles (~8 us) late.
+  // Problems that start together stay in phase for the whole solve, so every CU streams history
+  // rows at the same time (HBM-bound) and evaluates the objective at the same time (VALU-bound);
+  // offsetting half the chip by part of an iteration lets one half's stream run while the other
+  // half evaluates.  C2 (B = 1024): +6% on two boxes, +0.4% on a third; C3 (16 problems per slot)
+  // gets no stagger
+  // (profiles/r02_ab_stagger.log).  Results are unchanged (timing only).
+  if (a.stagger > 0 && (blockIdx.x & 1)) {
+    const unsigned long long t0 = clock64();
+    while (clock64() - t0 < (unsigned long long)a.stagger) __builtin_amdgcn_s_sleep(8);
+  }
   for (int b = blockIdx.x;;) {
     if (a.queue) {
       __syncthreads();  // every thread is done with the previous problem's LDS image
@@ -1384,6 +1397,8 @@ extern "C" int dava_ba_solve_plan(const DavaScene* scene, const DavaSolverConfig
   return plan->lds_bytes > kMaxLds || kcap > kMaxCompactEntries ? DAVA_ERR_UNSUPPORTED : DAVA_OK;
 }
 
+constexpr int kStaggerCycles = 20000;  // ~8 us at the shader clock; one C2 iteration is ~47 us
+
 template <int MODE, bool GV, int RES, bool XL, int PPT, int NW>
 static void launch_solve_ppt(const SolveArgs& a, int B, int lds, hipStream_t s) {
   const auto kernel = bfgs_ba_solve_kernel<MODE, GV, RES, XL, PPT, NW>;
@@ -1392,13 +1407,20 @@ static void launch_solve_ppt(const SolveArgs& a, int B, int lds, hipStream_t s) 
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize, lds);
   int grid = B;
   SolveArgs args = a;
-  if (args.queue) {  // one workgroup per resident slot (host queries only; nothing synchronises)
+  int slots = 0;  // workgroups resident at once (host queries only; nothing synchronises)
+  {
     int dev = 0, cus = 0, per_cu = 0;
     if (hipGetDevice(&dev) == hipSuccess &&
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
         hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, threads, lds) == hipSuccess && per_cu > 0 &&
         cus > 0)
-      grid = min(B, per_cu * cus);
+      slots = per_cu * cus;
+  }
+  // stagger only a launch whose problems all run at once (one round, B <= slots)
+  args.stagger = slots > 0 && B <= slots && B > 1 ? kStaggerCycles : 0;
+  if (const char* e = getenv("DAVA_STAGGER")) args.stagger = max(0, atoi(e));  // A/B knob (cycles)
+  if (args.queue) {  // one workgroup per resident slot
+    if (slots > 0) grid = min(B, slots);
     // The hardware already refills a slot as soon as its workgroup retires, but only from its
     // own XCD's share of the grid (workgroups are dealt round-robin over the 8 XCDs): the
     // queue pays where per-problem work is uneven -- stopping rules active, or few problems
@@ -1504,6 +1526,7 @@ static int solve_impl(const DavaScene* scene, const DavaSolverConfig* config, co
   a.kcap = kcap;
   a.lcap = lcap;
   a.phase_cycles = nullptr;
+  a.stagger = 0;
   a.queue = queue ? reinterpret_cast<int*>(static_cast<char*>(workspace) + need) : nullptr;
   a.tape_x = a.tape_g = a.tape_s = nullptr;
   a.tape_T = tl.T;

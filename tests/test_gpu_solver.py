@@ -356,6 +356,21 @@ def test_work_queue_launch_is_bitwise_invisible(device, stopping, monkeypatch):
         assert st[:, 0].unique().numel() > 1
 
 
+def test_staggered_start_is_bitwise_invisible(device, monkeypatch):
+    """A launch whose problems are all resident at once starts its odd workgroups late (phases
+    spread over the chip); timing only -- every result and status word is bitwise the same."""
+    x0, obs, vis = _scene(256, 2, 128, False, 561)
+    kw = dict(iterations=40, error_threshold=-1.0, minimum_step=-1.0, hessian_mode="compact")
+    out, st = _gpu_solve(device, x0, obs, vis, 2, 128, False, **kw)
+    monkeypatch.setenv("DAVA_STAGGER", "0")
+    ref, st_ref = _gpu_solve(device, x0, obs, vis, 2, 128, False, **kw)
+    monkeypatch.setenv("DAVA_STAGGER", "200000")
+    late, st_late = _gpu_solve(device, x0, obs, vis, 2, 128, False, **kw)
+    monkeypatch.delenv("DAVA_STAGGER")
+    assert torch.equal(out, ref) and torch.equal(st, st_ref)
+    assert torch.equal(late, ref) and torch.equal(st_late, st_ref)
+
+
 @pytest.mark.parametrize("waves", ["1", "2", "4"])
 @pytest.mark.parametrize("m,n,distortion,k", [(2, 64, False, 20), (2, 128, False, 20), (4, 256, True, 20)])
 def test_workgroup_waves_match_oracle(device, m, n, distortion, k, waves, monkeypatch):
