@@ -54,15 +54,15 @@ constexpr int kAdjWaves = 4;
 constexpr int kAdjBlock = kWave * kAdjWaves;
 
 struct AdjointCarve {
-  int xb, sbp, gbp, db, gk, p1, p2, wb, hd, hw, sv, wv, yv, gv, sp0, sp1, sp2, sp3, sc, xd, gd, views, vpart, obsd,
-      obs, obsacc, scratch, vis_bytes_off, total_bytes;
+  int xb, sbp, gbp, db, gk, p1, p2, wb, hd, hw, sv, wv, yv, gv, sp0, sp1, sp2, sp3, ak, an, sc, xd, gd, views,
+      vpart, obsd, obs, obsacc, scratch, vis_bytes_off, total_bytes;
 };
 
 __host__ __device__ inline AdjointCarve carve_adjoint(int M, int N, int Pv, int T) {
   AdjointCarve c;
   int off = 0;
   int* vec[] = {&c.xb, &c.sbp, &c.gbp, &c.db, &c.gk, &c.p1, &c.p2, &c.wb, &c.hd, &c.hw,
-                &c.sv, &c.wv, &c.yv, &c.gv, &c.sp0, &c.sp1, &c.sp2, &c.sp3};
+                &c.sv, &c.wv, &c.yv, &c.gv, &c.sp0, &c.sp1, &c.sp2, &c.sp3, &c.ak, &c.an};
   for (int* v : vec) { *v = off; off += Pv; }
   c.sc = off; off += T;
   c.xd = off; off += 2 * Pv;  // Dual
@@ -91,11 +91,12 @@ __device__ __forceinline__ float dot4(f4a a, f4a b) {
 // Entries are dealt round-robin to the 4 waves (two in flight per wave); the wave partials are added
 // in the fixed order (w0 + w2) + (w1 + w3), then base * (v1 | v2).  out / v / spares: LDS vectors.
 // Ends with a barrier.
+// R1_j0: if not null, entry j0's R1 row comes from this LDS vector instead of R1 + j0 Pv.
 template <int GM, class Coef>
 __device__ __forceinline__ void pair_pass(int P, int Pv, int j0, int j1, const float* __restrict__ R1,
                                           const float* __restrict__ R2, const float* v1, const float* v2,
                                           float base, Coef coef, float* out1, float* out2, float* sp0, float* sp1,
-                                          float* sp2, float* sp3) {
+                                          float* sp2, float* sp3, const float* R1_j0 = nullptr) {
   const int lane = threadIdx.x & (kWave - 1);
   const int wave = threadIdx.x / kWave;
   const int G = (P + 3) / 4;
@@ -110,7 +111,8 @@ __device__ __forceinline__ void pair_pass(int P, int Pv, int j0, int j1, const f
 #pragma unroll
     for (int m = 0; m < GM; ++m) {
       const int q = lane + kWave * m;
-      r1[m] = ok[m] ? ldv(R1 + (size_t)j * Pv + 4 * q) : f4a{0, 0, 0, 0};
+      const float* r1p = R1_j0 && j == j0 ? R1_j0 : R1 + (size_t)j * Pv;
+      r1[m] = ok[m] ? ldv(r1p + 4 * q) : f4a{0, 0, 0, 0};
       r2[m] = ok[m] ? ldv(R2 + (size_t)j * Pv + 4 * q) : f4a{0, 0, 0, 0};
     }
   };
@@ -215,6 +217,10 @@ __global__ __launch_bounds__(kAdjBlock, 1) void bfgs_ba_adjoint_kernel(AdjointAr
   float* sp1 = lds + cv.sp1;
   float* sp2 = lds + cv.sp2;
   float* sp3 = lds + cv.sp3;
+  // a_k lives in LDS while step k updates it (ak) and -wbar_k waits there for step k - 1 (an); the
+  // workspace row a_k is written once, final, and only read by later steps (never read-modify-write)
+  float* akl = lds + cv.ak;
+  float* anl = lds + cv.an;
   float* sc = lds + cv.sc;
   Dual* xd = reinterpret_cast<Dual*>(lds + cv.xd);
   Dual* gd = reinterpret_cast<Dual*>(lds + cv.gd);
@@ -234,7 +240,7 @@ __global__ __launch_bounds__(kAdjBlock, 1) void bfgs_ba_adjoint_kernel(AdjointAr
 
   for (int i = tid; i < Pv; i += kAdjBlock) {
     xb[i] = i < P ? a.xbar[(size_t)b * P + i] : 0.f;
-    sbp[i] = gbp[i] = 0.f;
+    sbp[i] = gbp[i] = anl[i] = 0.f;
   }
   for (int i = tid; i < tl.T; i += kAdjBlock) sc[i] = a.tape[tl.scal + (size_t)b * tl.T + i];
   for (int i = tid; i < 2 * MN; i += kAdjBlock) {
@@ -266,7 +272,7 @@ __global__ __launch_bounds__(kAdjBlock, 1) void bfgs_ba_adjoint_kernel(AdjointAr
         yv[i] = g1 - g0;
         sv[i] = srow[i];
         wv[i] = wrow[i];
-        ak[i] = (k == n - 1 ? 0.f : ak[i]) - db[i];  // d_k = -H_k g_k adds -dbar_k g_k^T to H_k's adjoint
+        akl[i] = anl[i] - db[i];  // d_k = -H_k g_k adds -dbar_k g_k^T to H_k's adjoint
       }
       __syncthreads();
       const float rho = sc[K + k - 1], c = sc[2 * K + k - 1];
@@ -275,7 +281,7 @@ __global__ __launch_bounds__(kAdjBlock, 1) void bfgs_ba_adjoint_kernel(AdjointAr
                     [](int, float as, float gs, float aw, float gw, float& k1, float& k2, float& k3, float& k4) {
                       k1 = gs; k2 = as; k3 = gw; k4 = aw;
                     },
-                    p1, p2, sp0, sp1, sp2, sp3);
+                    p1, p2, sp0, sp1, sp2, sp3, akl);
       float r[7] = {0, 0, 0, 0, 0, 0, 0};
       for (int i = tid; i < P; i += kAdjBlock) {
         const float si = sv[i], wi = wv[i], yi = yv[i], di = db[i];
@@ -322,9 +328,9 @@ __global__ __launch_bounds__(kAdjBlock, 1) void bfgs_ba_adjoint_kernel(AdjointAr
         const float hk = hd[i] + e1 * sv[i] + e2 * wv[i];
         gk[i] = gbp[i] - hk + ybar;
         gbp[i] = -ybar;
-        const float af = ak[i] + wb[i];
-        ak[i] = af;
-        Ar[(size_t)(k - 1) * Pv + i] = -wb[i];
+        const float af = akl[i] + wb[i];
+        ak[i] = af;  // final a_k (read by the passes of steps < k)
+        anl[i] = -wb[i];
         tr[0] += af * gv[i];
         if (k == 1 && i < P) tr[0] -= wb[i] * g0r[i];  // a_0 = -wbar_1
       }

@@ -53,7 +53,22 @@ struct SolveArgs {
   float* tape_s;  // (B, tape_T)
   int tape_T;
   int stagger;    // shader cycles the odd workgroups wait before starting (0: none)
+  float drop_p;   // training-mode drop path probability (0: eval mode)
+  unsigned long long drop_seed;
 };
+
+// Training mode's drop path (bfgs_solver.py:121-125): problem b keeps updating at iteration k iff
+// u(seed, b, k) > p, u uniform on [0, 1) with 24-bit resolution from a counter-based 64-bit mix
+// (splitmix64's finaliser over the packed counter): no state, any launch shape or work-queue
+// order draws the same schedule.
+__device__ __forceinline__ float drop_uniform(unsigned long long seed, int b, int k) {
+  unsigned long long z = seed ^ (((unsigned long long)(unsigned)b << 32) | (unsigned)k);
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  return (float)(z >> 40) * (1.0f / 16777216.0f);
+}
 
 struct LdsCarve {
   int x, d, ge, g0, g1, s0, s1, hy0, hy1, hg, obs, views, vpart, scratch, hcoef, hrho, hc, hist, vis_bytes_off,
@@ -912,6 +927,10 @@ __global__ __launch_bounds__(kWave * NW, DAVA_SOLVE_WAVES_PER_EU) void bfgs_ba_s
     unsigned long long ph_t0 = ph_start;
   #endif
     for (int k = 0; k < a.iters; ++k) {
+      if (a.drop_p > 0.f && !(drop_uniform(a.drop_seed, b, k) > a.drop_p)) {  // uniform: same draw in every thread
+        reason = DAVA_STOP_DROP;
+        break;
+      }
       { float* t = g; g = gp; gp = t; }  // gp <- previous gradient; g <- (trial) gradient buffer
       if (a.tape_x) {  // recording: x_k (the same threads wrote x[i] when the last step was taken)
         float* r = a.tape_x + ((size_t)b * a.iters + k) * Pv;
@@ -1480,6 +1499,7 @@ static int solve_impl(const DavaScene* scene, const DavaSolverConfig* config, co
   int st = check_scene(scene);
   if (st != DAVA_OK) return st;
   if (!config || config->iterations < 0 || config->max_line_search_trials < 0) return DAVA_ERR_INVALID_ARGUMENT;
+  if (!(config->drop_path_p >= 0.f && config->drop_path_p <= 1.f)) return DAVA_ERR_INVALID_ARGUMENT;
   const int mode = config->hessian_mode;
   if (mode != DAVA_HESSIAN_DENSE && mode != DAVA_HESSIAN_COMPACT) return DAVA_ERR_INVALID_ARGUMENT;
   if (record && !tape_supported(scene, config)) return DAVA_ERR_UNSUPPORTED;
@@ -1527,6 +1547,8 @@ static int solve_impl(const DavaScene* scene, const DavaSolverConfig* config, co
   a.lcap = lcap;
   a.phase_cycles = nullptr;
   a.stagger = 0;
+  a.drop_p = config->drop_path_p;
+  a.drop_seed = ((unsigned long long)config->drop_seed_hi << 32) | config->drop_seed_lo;
   a.queue = queue ? reinterpret_cast<int*>(static_cast<char*>(workspace) + need) : nullptr;
   a.tape_x = a.tape_g = a.tape_s = nullptr;
   a.tape_T = tl.T;

@@ -20,8 +20,8 @@ DAVA_HESSIAN_DENSE = 0
 DAVA_HESSIAN_COMPACT = 1
 DAVA_RESIDUAL_SQUARED_REPROJECTION = 0
 DAVA_RESIDUAL_RAY_ANGLE = 1
-ABI_VERSION = 2  # include/dava_ba.h DAVA_ABI_VERSION
-STOP_ITERATIONS, STOP_ERROR, STOP_STEP = 0, 1, 2
+ABI_VERSION = 3  # include/dava_ba.h DAVA_ABI_VERSION
+STOP_ITERATIONS, STOP_ERROR, STOP_STEP, STOP_DROP = 0, 1, 2, 3
 STATUS_WORDS = 4
 
 _c_i64 = ctypes.c_int64
@@ -52,6 +52,9 @@ class DavaSolverConfig(ctypes.Structure):
         ("max_line_search_trials", _c_i32),
         ("strong_wolfe", _c_i32),
         ("hessian_mode", _c_i32),
+        ("drop_path_p", ctypes.c_float),
+        ("drop_seed_lo", ctypes.c_uint32),
+        ("drop_seed_hi", ctypes.c_uint32),
     ]
 
 

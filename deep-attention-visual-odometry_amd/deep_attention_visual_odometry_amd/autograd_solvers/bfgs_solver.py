@@ -89,12 +89,18 @@ class BFGSSolver(Module):
             error_threshold, num_iterations = self.training_error_threshold, self.training_iterations
         else:
             error_threshold, num_iterations = self.error_threshold, self.iterations
-        stochastic = self.training and (self.drop_path_p > 0.0 or self.return_second_last)
-        if isinstance(error_function, ReprojectionError) and not stochastic:
+        # training mode's drop path runs fused (counter-based draws, DAVA_STOP_DROP); the reference's
+        # return_second_last scatter (:196-212) moves rows between problems, so it stays generic
+        drop_p = self.drop_path_p if self.training else 0.0
+        generic_training = drop_p > 0.0 and bool(os.environ.get("DAVA_GENERIC_TRAINING"))  # torch-RNG generic loop
+        if isinstance(error_function, ReprojectionError) and not (self.training and self.return_second_last) \
+                and not generic_training:
+            seed = int(torch.randint(0, 2 ** 62, (1,)).item()) if drop_p > 0.0 else 0  # from torch's default generator
             if not parameters.requires_grad:
-                return self._fused(parameters, error_function, error_threshold, num_iterations)
+                return self._fused(parameters, error_function, error_threshold, num_iterations, drop_p, seed)
             if self._adjoint_available(parameters, error_function, num_iterations):
-                return self._fused_differentiable(parameters, error_function, error_threshold, num_iterations)
+                return self._fused_differentiable(parameters, error_function, error_threshold, num_iterations,
+                                                  drop_p, seed)
         return self._generic(parameters, error_function, error_threshold, num_iterations)
 
     def _adjoint_available(self, parameters, fn: ReprojectionError, num_iterations) -> bool:
@@ -108,7 +114,8 @@ class BFGSSolver(Module):
         return native_ops.solve_tape_supported(max(parameters.numel() // parameters.size(-1), 1), fn.num_views,
                                                fn.num_points, fn.distortion, num_iterations, fn.residual)
 
-    def _fused_differentiable(self, parameters, fn: ReprojectionError, error_threshold, num_iterations):
+    def _fused_differentiable(self, parameters, fn: ReprojectionError, error_threshold, num_iterations, drop_p=0.0,
+                              seed=0):
         lead = parameters.shape[:-1]
         if fn.batch_shape != lead:
             raise ValueError(f"ReprojectionError batch shape {tuple(fn.batch_shape)} != parameters {tuple(lead)}")
@@ -117,11 +124,12 @@ class BFGSSolver(Module):
             x0, fn.observations.reshape(-1, fn.num_views, fn.num_points, 2),
             fn.visibility.reshape(-1, fn.num_views, fn.num_points), fn.num_views, fn.num_points, fn.distortion,
             sufficient_decrease=self.sufficient_decrease, curvature=self.curvature, error_threshold=error_threshold,
-            iterations=num_iterations, minimum_step=self.minimum_step, residual=fn.residual)
+            iterations=num_iterations, minimum_step=self.minimum_step, residual=fn.residual, drop_path_p=drop_p,
+            drop_seed=seed)
         self.last_status = status
         return x.reshape(parameters.shape)
 
-    def _fused(self, parameters, fn: ReprojectionError, error_threshold, num_iterations):
+    def _fused(self, parameters, fn: ReprojectionError, error_threshold, num_iterations, drop_p=0.0, seed=0):
         lead = parameters.shape[:-1]
         if fn.batch_shape != lead:
             raise ValueError(f"ReprojectionError batch shape {tuple(fn.batch_shape)} != parameters {tuple(lead)}")
@@ -134,7 +142,7 @@ class BFGSSolver(Module):
             fn.visibility.reshape(-1, fn.num_views, fn.num_points), fn.num_views, fn.num_points, fn.distortion,
             sufficient_decrease=self.sufficient_decrease, curvature=self.curvature,
             error_threshold=error_threshold, iterations=num_iterations, minimum_step=self.minimum_step,
-            hessian_mode=mode, want_status=True, residual=fn.residual)
+            hessian_mode=mode, want_status=True, residual=fn.residual, drop_path_p=drop_p, drop_seed=seed)
         self.last_status = status
         return x.reshape(parameters.shape)
 

@@ -6,6 +6,7 @@ device.  The generic BFGS building blocks are ``torch.autograd.Function`` s whos
 backward are both ``torch.ops.dava`` operators, so ``torch.compile`` traces them (fake kernels
 give the shapes) and autograd differentiates through them like the reference's torch code.
 """
+import os
 from typing import Optional, Tuple
 
 import torch
@@ -71,15 +72,17 @@ def ba_solve(x0: torch.Tensor, observations: torch.Tensor, visibility: torch.Ten
              error_threshold: float = 1e-4, iterations: int = 1000, minimum_step: float = 1e-8,
              max_line_search_trials: int = 1000, strong: bool = True, hessian_mode: int = N.DAVA_HESSIAN_DENSE,
              want_error: bool = False, want_status: bool = False, workspace: Optional[torch.Tensor] = None,
-             residual: int = N.DAVA_RESIDUAL_SQUARED_REPROJECTION):
-    """One fused launch for the whole batch (``torch.ops.dava.ba_solve``).  Returns (x, error|None, status|None)."""
+             residual: int = N.DAVA_RESIDUAL_SQUARED_REPROJECTION, drop_path_p: float = 0.0, drop_seed: int = 0):
+    """One fused launch for the whole batch (``torch.ops.dava.ba_solve``).  Returns (x, error|None, status|None).
+    ``drop_path_p`` > 0: training mode's drop path with the counter-based schedule of ``drop_seed``."""
     x0 = _fp32_on_device(x0, "parameters")
     obs, vis = _scene_inputs(x0, observations, visibility)
     x, err, status = torch.ops.dava.ba_solve(
         x0, obs, vis, int(num_views), int(num_points), bool(distortion), float(sufficient_decrease),
         float(curvature), float(error_threshold), int(iterations), float(minimum_step), int(max_line_search_trials),
         bool(strong), int(hessian_mode), int(residual), bool(want_error),
-        workspace if workspace is not None else x0.new_empty((0,), dtype=torch.uint8))
+        workspace if workspace is not None else x0.new_empty((0,), dtype=torch.uint8), float(drop_path_p),
+        int(drop_seed))
     return x, (err if want_error else None), (status if want_status else None)
 
 
@@ -92,6 +95,9 @@ def solve_tape_supported(batch: int, num_views: int, num_points: int, distortion
     return int(lib.dava_ba_solve_tape_bytes(sc, cfg)) > 0
 
 
+LAST_TAPE = None
+
+
 class _FusedSolve(torch.autograd.Function):
     """x_out = solve(x0, obs) in one recording launch; its backward is the adjoint kernel
     (csrc/bfgs_adjoint.hip), which replays the tape: the reference's create_graph gradient
@@ -100,15 +106,21 @@ class _FusedSolve(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x0, observations, visibility, num_views, num_points, distortion, residual, cfg):
-        c1, c2, thr, iters, min_step, trials, strong = cfg
+        c1, c2, thr, iters, min_step, trials, strong, drop_p, drop_seed = cfg
         x0c = _fp32_on_device(x0, "parameters")
         obs, vis = _scene_inputs(x0c, observations, visibility)
         x, status, tape = torch.ops.dava.ba_solve_record(
             x0c, obs, vis, int(num_views), int(num_points), bool(distortion), float(c1), float(c2), float(thr),
-            int(iters), float(min_step), int(trials), bool(strong), int(residual))
+            int(iters), float(min_step), int(trials), bool(strong), int(residual), float(drop_p), int(drop_seed))
         ctx.save_for_backward(tape, status, obs, vis)
+        if os.environ.get("DAVA_STASH_TAPE"):  # diagnostic: the last recording's tape, for tools/
+            global LAST_TAPE
+            LAST_TAPE = tape
         ctx.meta = (int(num_views), int(num_points), bool(distortion), int(iters), int(residual))
         ctx.mark_non_differentiable(status)
+        ctx.recorded = torch.cuda.Event()  # the tape is complete once the recording launch is
+        ctx.recorded.record(torch.cuda.current_stream(x0c.device))
+        ctx.fwd_stream = torch.cuda.current_stream(x0c.device).cuda_stream
         return x, status
 
     @staticmethod
@@ -119,8 +131,19 @@ class _FusedSolve(torch.autograd.Function):
         need_x, need_obs = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
         if x_grad is None:
             return (None,) * 8
+        # autograd may run this backward on another stream than the recording launch's: order the
+        # adjoint after the tape is written
+        cur = torch.cuda.current_stream(tape.device)
+        if os.environ.get("DAVA_DEBUG_STREAMS"):
+            print(f"[dava] adjoint stream {cur.cuda_stream:#x}, recording stream {ctx.fwd_stream:#x}", flush=True)
+        if not os.environ.get("DAVA_NO_ADJOINT_WAIT"):
+            cur.wait_event(ctx.recorded)
+        if os.environ.get("DAVA_SYNC_BEFORE_BACKWARD"):  # diagnostic
+            torch.cuda.synchronize(tape.device)
         gx, gobs = torch.ops.dava.ba_solve_backward(_c(x_grad.to(torch.float32)), tape, status, obs, vis, m, n, dist,
                                                     iters, residual, bool(need_obs))
+        if os.environ.get("DAVA_SYNC_AFTER_BACKWARD"):  # diagnostic
+            torch.cuda.synchronize(tape.device)
         return (gx if need_x else None, gobs if need_obs else None, None, None, None, None, None, None)
 
 
@@ -128,10 +151,12 @@ def ba_solve_differentiable(x0: torch.Tensor, observations: torch.Tensor, visibi
                             num_points: int, distortion: bool, *, sufficient_decrease: float = 1e-4,
                             curvature: float = 0.9, error_threshold: float = 1e-4, iterations: int = 1000,
                             minimum_step: float = 1e-8, max_line_search_trials: int = 1000, strong: bool = True,
-                            residual: int = N.DAVA_RESIDUAL_SQUARED_REPROJECTION):
+                            residual: int = N.DAVA_RESIDUAL_SQUARED_REPROJECTION, drop_path_p: float = 0.0,
+                            drop_seed: int = 0):
     """The fused COMPACT solve as an autograd node w.r.t. x0 and the observations.
     Returns (x, status)."""
-    cfg = (sufficient_decrease, curvature, error_threshold, iterations, minimum_step, max_line_search_trials, strong)
+    cfg = (sufficient_decrease, curvature, error_threshold, iterations, minimum_step, max_line_search_trials, strong,
+           drop_path_p, drop_seed)
     return _FusedSolve.apply(x0, observations, visibility, num_views, num_points, distortion, residual, cfg)
 
 

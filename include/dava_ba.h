@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define DAVA_ABI_VERSION 2
+#define DAVA_ABI_VERSION 3
 
 enum DavaStatus {
   DAVA_OK = 0,
@@ -55,7 +55,8 @@ enum DavaHessianMode {
 enum DavaStopReason {
   DAVA_STOP_ITERATIONS = 0, /* ran `iterations` steps                 */
   DAVA_STOP_ERROR = 1,      /* error <= error_threshold (or NaN)      */
-  DAVA_STOP_STEP = 2        /* ||step|| <= minimum_step (or NaN)      */
+  DAVA_STOP_STEP = 2,       /* ||step|| <= minimum_step (or NaN)      */
+  DAVA_STOP_DROP = 3        /* training-mode drop path (drop_path_p)  */
 };
 
 /* Per-(view, point) residual summed into the objective.
@@ -94,6 +95,12 @@ typedef struct DavaSolverConfig {
   int32_t max_line_search_trials; /* 1000 in wolfe_conditions.py:116           */
   int32_t strong_wolfe;           /* 1 (bfgs_solver.py:189)                    */
   int32_t hessian_mode;           /* DavaHessianMode                           */
+  /* Training mode's drop path (bfgs_solver.py:121-125): at the top of every iteration a problem
+   * keeps updating only if a uniform draw in [0, 1) exceeds drop_path_p, else it stops for good
+   * (DAVA_STOP_DROP).  Draws are counter-based (seed, problem, iteration): the same seed gives the
+   * same schedule on any launch shape.  0 = eval mode (the default).                           */
+  float drop_path_p;
+  uint32_t drop_seed_lo, drop_seed_hi;
 } DavaSolverConfig;
 
 /* Per-problem status written by dava_ba_solve: int32 (B, 4) =

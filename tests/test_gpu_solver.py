@@ -537,3 +537,54 @@ def test_nan_problem_does_not_disturb_its_neighbours(device):
                         minimum_step=-1.0)
     assert torch.equal(out[[0, 2, 3]], clean[[0, 2, 3]])
     assert not torch.isfinite(out[1]).all()
+
+
+# ---- training mode's drop path in the fused kernel (bfgs_solver.py:121-125) ----
+
+def _train_solve(device, x0, obs, vis, m, n, p, k, seed):
+    from deep_attention_visual_odometry_amd import BFGSSolver, ReprojectionError
+
+    s = BFGSSolver(drop_path_p=p, training_iterations=k, training_error_threshold=-1.0, minimum_step=-1.0)
+    assert s.training
+    torch.manual_seed(seed)
+    out = s(x0.to(device), ReprojectionError(obs.to(device), vis.to(device), m, n)).cpu()
+    return out, s.last_status.cpu()
+
+
+def test_fused_drop_path_schedule_is_geometric(device):
+    """Every iteration a problem keeps updating with probability 1 - p (reference: updating &=
+    rand_like > p): the number of steps is geometric, truncated at K.  Statistical parity --
+    the kernel draws from its own counter-based generator, not torch's stream."""
+    p, k, b = 0.1, 30, 4096
+    x0, obs, vis = _scene(b, 2, 64, False, 571)
+    _, st = _train_solve(device, x0, obs, vis, 2, 64, p, k, 5)
+    steps = st[:, 0].double()
+    expect = [(1 - p) ** j * p for j in range(k)] + [(1 - p) ** k]
+    hist = torch.bincount(st[:, 0].long(), minlength=k + 1).double() / b
+    mean = sum(j * e for j, e in enumerate(expect))
+    var = sum((j - mean) ** 2 * e for j, e in enumerate(expect))
+    assert abs(steps.mean().item() - mean) < 4 * (var / b) ** 0.5
+    assert (hist - torch.tensor(expect, dtype=torch.float64)).abs().max() < 0.02
+    assert ((st[:, 0] < k) == (st[:, 1] == 3)).all()  # DAVA_STOP_DROP exactly for the dropped ones
+    # seeded through torch's default generator: same seed, same schedule; another seed, another one
+    _, st2 = _train_solve(device, x0, obs, vis, 2, 64, p, k, 5)
+    _, st3 = _train_solve(device, x0, obs, vis, 2, 64, p, k, 6)
+    assert torch.equal(st, st2) and not torch.equal(st[:, 0], st3[:, 0])
+
+
+def test_fused_drop_path_is_the_eval_solve_stopped_early(device):
+    """A dropped problem returns exactly the eval-mode solve run for the steps it took."""
+    from deep_attention_visual_odometry_amd import native_ops
+
+    x0, obs, vis = _scene(96, 2, 128, False, 572)
+    out, st = _train_solve(device, x0, obs, vis, 2, 128, 0.15, 25, 11)
+    assert st[:, 0].unique().numel() > 3
+    for steps in st[:, 0].unique().tolist():
+        idx = (st[:, 0] == steps).nonzero().flatten()
+        if steps == 0:
+            assert torch.equal(out[idx], x0[idx])
+            continue
+        ref, _, _ = native_ops.ba_solve(x0[idx].to(device), obs[idx].to(device), vis[idx].to(device), 2, 128, False,
+                                        iterations=int(steps), error_threshold=-1.0, minimum_step=-1.0,
+                                        hessian_mode=1)
+        assert torch.equal(out[idx], ref.cpu()), steps

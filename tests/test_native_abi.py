@@ -45,7 +45,7 @@ def test_python_binding_types_every_declared_symbol():
 
 def test_library_is_built_for_gfx950(lib):
     assert lib.dava_device_arch() == b"gfx950"
-    assert lib.dava_abi_version() == 2
+    assert lib.dava_abi_version() == 3
     blob = open(lib._name, "rb").read()
     assert b"gfx950" in blob
 
