@@ -70,6 +70,9 @@ def parse(argv=None):
     p.add_argument("--cpu-sample", type=int, default=16,
                    help="problems per timed CPU-oracle run (3 runs on disjoint slices; 0 = skip)")
     p.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "pmc_traffic.json"))
+    p.add_argument("--differentiate", action="store_true",
+                   help="time the solve AND its gradient (recording solve + adjoint kernel, d(w.x)/d(x0, obs)) -- "
+                        "the reference's create_graph mode; not the headline metric")
     p.add_argument("--launch-test", action="store_true",
                    help="multi-rank LAUNCH plumbing check on CPU (gloo, identity stub instead of the solve); "
                         "prints a line marked as a launch test, never a measurement")
@@ -275,6 +278,24 @@ def main():
                                                want_status=True, workspace=workspace, residual=residual)
             return x, status
 
+        if args.differentiate:  # recording solve + adjoint, each timed with its own events
+            cot = torch.randn(x0.shape, generator=torch.Generator().manual_seed(1)).to(dev)
+            phase_ms = []
+
+            def solve():  # noqa: F811
+                ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+                ev[0].record()
+                x, status, tape = torch.ops.dava.ba_solve_record(
+                    x0, obs, vis, args.views, args.points, distortion, 1e-4, 0.9, args.error_threshold,
+                    args.iterations, args.minimum_step, 1000, True, residual)
+                ev[1].record()
+                gx, gobs = torch.ops.dava.ba_solve_backward(cot, tape, status, obs, vis, args.views, args.points,
+                                                            distortion, args.iterations, residual, True)
+                ev[2].record()
+                phase_ms.append(ev)
+                solve.grads = (gx, gobs)
+                return x, status
+
         def sync():
             torch.cuda.synchronize(dev)
 
@@ -336,12 +357,54 @@ def main():
                         for r in range(world)]
                 base["config"]["gathered_matches_inputs"] = bool(torch.equal(x_all, torch.cat(want)))
             print(json.dumps(base), flush=True)
+        elif args.differentiate:
+            print(json.dumps(differentiate_line(args, base, world, b, p, distortion, ray, phase_ms[-args.steps:],
+                                                st, finite, solve.grads)), flush=True)
         else:
             print(json.dumps(measurement_line(args, base, world, b, p, mn, distortion, ray, plan, kernel_ms, st,
                                               finite, x0_cpu, obs_cpu, vis_cpu, x)), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def adjoint_algorithmic_bytes(p: int, n: int) -> float:
+    """Minimum HBM bytes of the adjoint kernel for one problem of n steps (csrc/bfgs_adjoint.hip):
+    reverse step k reads rows (a_j, g_j), j = k .. n-1, and history rows (s_j, w_j), j < k-1, once each,
+    plus x_k, g_k, g_{k-1}, s_{k-1}, w_{k-1} and the final a_k write: Pv floats per row."""
+    pv = (p + 3) // 4 * 4
+    rows = sum(2 * (n - k) + 2 * max(k - 1, 0) + 6 for k in range(1, n)) + 2
+    return 4.0 * pv * rows
+
+
+def differentiate_line(args, line, world, b, p, distortion, ray, phase_ms, st, finite, grads):
+    fwd = float(np.mean([e[0].elapsed_time(e[1]) for e in phase_ms]))
+    bwd = float(np.mean([e[1].elapsed_time(e[2]) for e in phase_ms]))
+    algo = b * adjoint_algorithmic_bytes(p, args.iterations)
+    achieved = algo / (bwd * 1e-3) / 1e9
+    gx, gobs = grads
+    line.update({
+        "metric": f"BA problems/sec THROUGH the solve and its gradient (B={b} per GPU, {args.views} views x "
+                  f"{args.points} pts{', Brown-Conrady' if distortion else ''}{', ray-angle residual' if ray else ''}, "
+                  f"K={args.iterations}; d(w . x_K)/d(x0, observations))",
+        "dtype": "f32",
+        "data": "synthetic (seeded look-at scenes, x0 = truth + noise), fixed random cotangent w",
+        "config": {"workload": f"differentiate: batch={b} per GPU, {args.views}x{args.points}, P={p}, K={args.iterations} "
+                               f"fixed iterations, recording solve + adjoint",
+                   "global_batch": world * b, "num_parameters": p, "iterations": args.iterations,
+                   "parallelism": f"dp{world}"},
+        "phases_ms": {"recording_solve": round(fwd, 3), "adjoint": round(bwd, 3)},
+        "roofline": {"kernel": "bfgs_ba_adjoint_kernel", "bound": "hbm", "achieved": round(achieved, 1),
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                     "byte_model": "adjoint: per reverse step k, rows (a_j, g_j) j >= k and history rows (s_j, w_j) "
+                                   "j < k-1 read once + 6 tape/workspace rows; its dual-number HVP is on top",
+                     "algorithmic_bytes_per_launch": algo, "avg_launch_ms": round(bwd, 3)},
+        "cpu_baseline": None,
+        "parity": {"note": "gradient parity vs oracle autograd / the reference's goldens: tests/test_gpu_solve_grad.py"},
+        "diagnostics": {"all_finite": finite and bool(torch.isfinite(gx).all()) and bool(torch.isfinite(gobs).all()),
+                        "mean_steps_per_problem": round(st[:, 0].double().mean().item(), 2)},
+    })
+    return line
 
 
 def measurement_line(args, line, world, b, p, mn, distortion, ray, plan, kernel_ms, st, finite, x0_cpu, obs_cpu,

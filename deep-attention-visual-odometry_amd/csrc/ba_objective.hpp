@@ -203,7 +203,8 @@ template <bool GRAD, bool SLOPE, bool TRIAL, bool DOT = false, bool CHECK = fals
           int RES = DAVA_RESIDUAL_SQUARED_REPROJECTION, typename S = float, int NW = kWaves, int PPT = 0>
 __device__ __forceinline__ bool ba_eval(const Layout& L, const S* x, const S* d, float alpha, const float* obs,
                                         const uint8_t* vis, S* grad, S* views, S* vpart, float* scratch, int& buf,
-                                        S& E_out, S& slope_out, S* obs_grad = nullptr) {
+                                        S& E_out, S& slope_out, S* obs_grad = nullptr,
+                                        float* obs_tangent_acc = nullptr) {
   constexpr int BLOCK = kWave * NW;  // threads in the workgroup
   static_assert(!DOT || (GRAD && !SLOPE), "DOT derives the slope from the reverse-mode gradient");
   static_assert(!CHECK || TRIAL, "CHECK needs a trial point");
@@ -470,10 +471,14 @@ __device__ __forceinline__ bool ba_eval(const Layout& L, const S* x, const S* d,
                                        go0, go1);
       }
       if constexpr (GRAD && !std::is_same<S, float>::value) {
+        const int pr = m * N + n;
         if (obs_grad) {
-          const int pr = m * N + n;
           obs_grad[2 * pr] = go0;
           obs_grad[2 * pr + 1] = go1;
+        }
+        if (obs_tangent_acc) {  // (d2E/dobs dx) v added straight into a float accumulator (one owner per pair)
+          obs_tangent_acc[2 * pr] += go0.t;
+          obs_tangent_acc[2 * pr + 1] += go1.t;
         }
       }
       if constexpr (GRAD) {

@@ -54,22 +54,20 @@ constexpr int kAdjWaves = 4;
 constexpr int kAdjBlock = kWave * kAdjWaves;
 
 struct AdjointCarve {
-  int xb, sbp, gbp, db, gk, p1, p2, wb, hd, hw, sv, wv, yv, gv, sp0, sp1, sp2, sp3, ak, an, sc, xd, gd, views,
-      vpart, obsd, obs, obsacc, scratch, vis_bytes_off, total_bytes;
+  int xb, sbp, gbp, db, gk, p1, p2, wb, sv, wv, yv, gv, ak, an, sc, xd, gd, views, vpart, obs, obsacc, scratch,
+      vis_bytes_off, total_bytes;
 };
 
 __host__ __device__ inline AdjointCarve carve_adjoint(int M, int N, int Pv, int T) {
   AdjointCarve c;
   int off = 0;
-  int* vec[] = {&c.xb, &c.sbp, &c.gbp, &c.db, &c.gk, &c.p1, &c.p2, &c.wb, &c.hd, &c.hw,
-                &c.sv, &c.wv, &c.yv, &c.gv, &c.sp0, &c.sp1, &c.sp2, &c.sp3, &c.ak, &c.an};
+  int* vec[] = {&c.xb, &c.sbp, &c.gbp, &c.db, &c.gk, &c.p1, &c.p2, &c.wb, &c.sv, &c.wv, &c.yv, &c.gv, &c.ak, &c.an};
   for (int* v : vec) { *v = off; off += Pv; }
   c.sc = off; off += T;
   c.xd = off; off += 2 * Pv;  // Dual
   c.gd = off; off += 2 * Pv;  // Dual
   c.views = off; off += 2 * round_up(views_floats(M), 4);
   c.vpart = off; off += 2 * round_up(vpart_floats(M, kAdjWaves), 4);
-  c.obsd = off; off += 2 * 2 * M * N;  // Dual dE/dobs per (view, point)
   c.obs = off; off += round_up(2 * M * N, 4);
   c.obsacc = off; off += round_up(2 * M * N, 4);
   c.scratch = off; off += 2 * kAdjWaves * 32;
@@ -191,6 +189,8 @@ __device__ __forceinline__ void pair_pass(int P, int Pv, int j0, int j1, const f
   __syncthreads();
 }
 
+// One workgroup per CU: at two (the C3 image is 78 KB, it would fit) the 256-VGPR cap spills 100-165
+// registers of the dual-number evaluation and the kernel ran 39% slower (148.6 -> 206.9 ms at C3).
 template <int RES, int GM>
 __global__ __launch_bounds__(kAdjBlock, 1) void bfgs_ba_adjoint_kernel(AdjointArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -207,16 +207,19 @@ __global__ __launch_bounds__(kAdjBlock, 1) void bfgs_ba_adjoint_kernel(AdjointAr
   float* p1 = lds + cv.p1;
   float* p2 = lds + cv.p2;
   float* wb = lds + cv.wb;
-  float* hd = lds + cv.hd;
-  float* hw = lds + cv.hw;
+  // H_{k-1} dbar, H_{k-1} wbar: p1 is dead once wbar / sbar are formed, gk until the final loop
+  // (which reads hw[i] before it writes gk[i], in the same thread)
+  float* hd = p1;
+  float* hw = lds + cv.gk;
   float* sv = lds + cv.sv;
   float* wv = lds + cv.wv;
   float* yv = lds + cv.yv;
   float* gv = lds + cv.gv;
-  float* sp0 = lds + cv.sp0;
-  float* sp1 = lds + cv.sp1;
-  float* sp2 = lds + cv.sp2;
-  float* sp3 = lds + cv.sp3;
+  // the passes' cross-wave spares live in the dual vectors' space (dead until the HVP)
+  float* sp0 = lds + cv.xd;
+  float* sp1 = sp0 + Pv;
+  float* sp2 = lds + cv.gd;
+  float* sp3 = sp2 + Pv;
   // a_k lives in LDS while step k updates it (ak) and -wbar_k waits there for step k - 1 (an); the
   // workspace row a_k is written once, final, and only read by later steps (never read-modify-write)
   float* akl = lds + cv.ak;
@@ -226,7 +229,6 @@ __global__ __launch_bounds__(kAdjBlock, 1) void bfgs_ba_adjoint_kernel(AdjointAr
   Dual* gd = reinterpret_cast<Dual*>(lds + cv.gd);
   Dual* views = reinterpret_cast<Dual*>(lds + cv.views);
   Dual* vpart = reinterpret_cast<Dual*>(lds + cv.vpart);
-  Dual* obsd = reinterpret_cast<Dual*>(lds + cv.obsd);
   float* obs = lds + cv.obs;
   float* obsacc = lds + cv.obsacc;
   float* scratch = lds + cv.scratch;
@@ -361,9 +363,8 @@ __global__ __launch_bounds__(kAdjBlock, 1) void bfgs_ba_adjoint_kernel(AdjointAr
     __syncthreads();
     Dual E(0.f), unused(0.f);
     ba_eval<true, false, false, false, false, RES, Dual, kAdjWaves>(L, xd, nullptr, 0.f, obs, vis, gd, views, vpart,
-                                                                   scratch, buf, E, unused, obsd);
+                                                                   scratch, buf, E, unused, nullptr, obsacc);
     for (int i = tid; i < P; i += kAdjBlock) xb[i] += gd[i].t;
-    for (int i = tid; i < 2 * MN; i += kAdjBlock) obsacc[i] += obsd[i].t;
     __syncthreads();
   }
   for (int i = tid; i < P; i += kAdjBlock) a.x0_grad[(size_t)b * P + i] = xb[i];
