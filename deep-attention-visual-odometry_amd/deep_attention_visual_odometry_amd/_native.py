@@ -125,6 +125,8 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
                 "(or __graft_entry__.build()); there is no CPU fallback")
         lib = ctypes.CDLL(path)
         for name, (res, args) in SIGNATURES.items():
+            if os.environ.get("DAVA_LIB") and not hasattr(lib, name):
+                continue  # an older A/B build (tools/build_prev.sh) may predate some entry points
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args

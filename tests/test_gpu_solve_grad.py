@@ -414,5 +414,6 @@ def test_fused_adjoint_through_a_training_mode_solve(device):
             continue
         _, gx_ref, go_ref = _oracle_grads(x0[idx], obs[idx], vis[idx], 2, 64, False, w[idx], iterations=int(steps),
                                           error_threshold=-1.0, minimum_step=-1.0)
-        assert _rows_rel(xd.grad.cpu()[idx], gx_ref).max() <= 2e-3, steps
+        assert _rows_rel(xd.grad.cpu()[idx], gx_ref).max() <= 2e-3, (steps, idx.tolist(),
+                                                                      _rows_rel(xd.grad.cpu()[idx], gx_ref).tolist())
         assert _rows_rel(od.grad.cpu()[idx], go_ref).max() <= 2e-3, steps

@@ -10,7 +10,7 @@ mkdir -p "$T/csrc" "$T/include"
 for f in $(git -C "$R" ls-tree --name-only "$REV" deep-attention-visual-odometry_amd/csrc/); do
   git -C "$R" show "$REV:$f" > "$T/csrc/$(basename "$f")"
 done
-git -C "$R" show "$REV:include/dava_ba.h" > "$T/include/dava_ba.h"
+if [ -n "${CURRENT_HEADER:-}" ]; then cp "$R/include/dava_ba.h" "$T/include/"; else git -C "$R" show "$REV:include/dava_ba.h" > "$T/include/dava_ba.h"; fi
 OUT=$R/deep-attention-visual-odometry_amd/build/var_$NAME
 mkdir -p "$OUT"
 objs=()
