@@ -134,12 +134,20 @@ struct RayAngle {
 };
 constexpr float kRayEps = 2.220446049250313e-16f;
 
+// DAVA_RAY_RCP: divide by a norm as a multiplication by its reciprocal (one IEEE division per norm
+// instead of one per component: ~16 -> 7 division sequences per (view, point) pair).  Results move
+// by an ulp against torch's per-component division; 0 restores the component-wise form.
+#ifndef DAVA_RAY_RCP
+#define DAVA_RAY_RCP 1
+#endif
 // unit vector x / clamp(|x|, eps) and the projection of a cotangent / tangent through it
+// (inv_n = 1 / n, used when DAVA_RAY_RCP)
 template <typename S>
-__device__ __forceinline__ void ray_unit_backward(S r, S n, const S (&u)[3], const S (&g)[3], S (&out)[3]) {
+__device__ __forceinline__ void ray_unit_backward(S r, S n, S inv_n, const S (&u)[3], const S (&g)[3],
+                                                  S (&out)[3]) {
   const S k = r >= kRayEps ? u[0] * g[0] + u[1] * g[1] + u[2] * g[2] : S(0.0f);
 #pragma unroll
-  for (int c = 0; c < 3; ++c) out[c] = (g[c] - u[c] * k) / n;
+  for (int c = 0; c < 3; ++c) out[c] = DAVA_RAY_RCP ? (g[c] - u[c] * k) * inv_n : (g[c] - u[c] * k) / n;
 }
 
 template <bool GRAD, bool SLOPE, typename S>
@@ -150,34 +158,45 @@ __device__ __forceinline__ void ray_angle_pair(const RayAngle<S>& ra, const floa
   const S h[3] = {ob[0] - ra.cx, ob[1] - ra.cy, ra.F};
   const S hr = sqrt_(h[0] * h[0] + h[1] * h[1] + h[2] * h[2]);
   const S hn = clamp_min(hr, kRayEps);
-  const S a[3] = {h[0] / hn, h[1] / hn, h[2] / hn};
   const S pr = sqrt_(p0 * p0 + p1 * p1 + p2 * p2);
   const S pn = clamp_min(pr, kRayEps);
-  const S b[3] = {p0 / pn, p1 / pn, p2 / pn};
+  const S ihn = DAVA_RAY_RCP ? 1.0f / hn : S(0.0f), ipn = DAVA_RAY_RCP ? 1.0f / pn : S(0.0f);
+  const S a[3] = {DAVA_RAY_RCP ? h[0] * ihn : h[0] / hn, DAVA_RAY_RCP ? h[1] * ihn : h[1] / hn,
+                  DAVA_RAY_RCP ? h[2] * ihn : h[2] / hn};
+  const S b[3] = {DAVA_RAY_RCP ? p0 * ipn : p0 / pn, DAVA_RAY_RCP ? p1 * ipn : p1 / pn,
+                  DAVA_RAY_RCP ? p2 * ipn : p2 / pn};
   const S su[3] = {a[0] + b[0], a[1] + b[1], a[2] + b[2]};
   const S df[3] = {a[0] - b[0], a[1] - b[1], a[2] - b[2]};
   const S Sn = sqrt_(su[0] * su[0] + su[1] * su[1] + su[2] * su[2]);
   const S Dn = sqrt_(df[0] * df[0] + df[1] * df[1] + df[2] * df[2]);
   e += 2.0f * atan2_(Dn, Sn) * wgt;
   const S den = Sn * Sn + Dn * Dn;
+  // reciprocals shared by the forward (slope) and reverse (gradient) parts
+  const S iden = DAVA_RAY_RCP && (GRAD || SLOPE) ? 1.0f / den : S(0.0f);
+  const S iSn = DAVA_RAY_RCP && (GRAD || SLOPE) && Sn > 0.0f ? 1.0f / Sn : S(0.0f);
+  const S iDn = DAVA_RAY_RCP && (GRAD || SLOPE) && Dn > 0.0f ? 1.0f / Dn : S(0.0f);
   if constexpr (SLOPE) {
     const S dh[3] = {-ra.dcx, -ra.dcy, ra.dF};
     const S dp[3] = {dp0, dp1, dp2};
     S da[3], db[3];
-    ray_unit_backward(hr, hn, a, dh, da);  // the Jacobian of x -> x/|x| is symmetric
-    ray_unit_backward(pr, pn, b, dp, db);
-    const S dS = Sn > 0.0f ? (su[0] * (da[0] + db[0]) + su[1] * (da[1] + db[1]) + su[2] * (da[2] + db[2])) / Sn : S(0.0f);
-    const S dD = Dn > 0.0f ? (df[0] * (da[0] - db[0]) + df[1] * (da[1] - db[1]) + df[2] * (da[2] - db[2])) / Dn : S(0.0f);
-    sl += 2.0f * wgt * (Sn * dD - Dn * dS) / den;
+    ray_unit_backward(hr, hn, ihn, a, dh, da);  // the Jacobian of x -> x/|x| is symmetric
+    ray_unit_backward(pr, pn, ipn, b, dp, db);
+    const S nS = su[0] * (da[0] + db[0]) + su[1] * (da[1] + db[1]) + su[2] * (da[2] + db[2]);
+    const S nD = df[0] * (da[0] - db[0]) + df[1] * (da[1] - db[1]) + df[2] * (da[2] - db[2]);
+    const S dS = Sn > 0.0f ? (DAVA_RAY_RCP ? nS * iSn : nS / Sn) : S(0.0f);
+    const S dD = Dn > 0.0f ? (DAVA_RAY_RCP ? nD * iDn : nD / Dn) : S(0.0f);
+    sl += DAVA_RAY_RCP ? 2.0f * wgt * (Sn * dD - Dn * dS) * iden : 2.0f * wgt * (Sn * dD - Dn * dS) / den;
   }
   if constexpr (GRAD) {
-    const S gD = 2.0f * wgt * Sn / den, gS = -2.0f * wgt * Dn / den;  // atan2 backward
-    const S cD = Dn > 0.0f ? gD / Dn : S(0.0f), cS = Sn > 0.0f ? gS / Sn : S(0.0f);
+    const S gD = DAVA_RAY_RCP ? 2.0f * wgt * Sn * iden : 2.0f * wgt * Sn / den;  // atan2 backward
+    const S gS = DAVA_RAY_RCP ? -2.0f * wgt * Dn * iden : -2.0f * wgt * Dn / den;
+    const S cD = Dn > 0.0f ? (DAVA_RAY_RCP ? gD * iDn : gD / Dn) : S(0.0f);
+    const S cS = Sn > 0.0f ? (DAVA_RAY_RCP ? gS * iSn : gS / Sn) : S(0.0f);
     const S ga[3] = {cS * su[0] + cD * df[0], cS * su[1] + cD * df[1], cS * su[2] + cD * df[2]};
     const S gb[3] = {cS * su[0] - cD * df[0], cS * su[1] - cD * df[1], cS * su[2] - cD * df[2]};
     S gh[3], gp[3];
-    ray_unit_backward(hr, hn, a, ga, gh);
-    ray_unit_backward(pr, pn, b, gb, gp);
+    ray_unit_backward(hr, hn, ihn, a, ga, gh);
+    ray_unit_backward(pr, pn, ipn, b, gb, gp);
     gin[0] += gh[2] * ra.Fp;
     gin[1] -= gh[0];
     gin[2] -= gh[1];
