@@ -6,7 +6,6 @@ device.  The generic BFGS building blocks are ``torch.autograd.Function`` s whos
 backward are both ``torch.ops.dava`` operators, so ``torch.compile`` traces them (fake kernels
 give the shapes) and autograd differentiates through them like the reference's torch code.
 """
-import os
 from typing import Optional, Tuple
 
 import torch
@@ -95,9 +94,6 @@ def solve_tape_supported(batch: int, num_views: int, num_points: int, distortion
     return int(lib.dava_ba_solve_tape_bytes(sc, cfg)) > 0
 
 
-LAST_TAPE = None
-
-
 class _FusedSolve(torch.autograd.Function):
     """x_out = solve(x0, obs) in one recording launch; its backward is the adjoint kernel
     (csrc/bfgs_adjoint.hip), which replays the tape: the reference's create_graph gradient
@@ -113,14 +109,10 @@ class _FusedSolve(torch.autograd.Function):
             x0c, obs, vis, int(num_views), int(num_points), bool(distortion), float(c1), float(c2), float(thr),
             int(iters), float(min_step), int(trials), bool(strong), int(residual), float(drop_p), int(drop_seed))
         ctx.save_for_backward(tape, status, obs, vis)
-        if os.environ.get("DAVA_STASH_TAPE"):  # diagnostic: the last recording's tape, for tools/
-            global LAST_TAPE
-            LAST_TAPE = tape
         ctx.meta = (int(num_views), int(num_points), bool(distortion), int(iters), int(residual))
         ctx.mark_non_differentiable(status)
         ctx.recorded = torch.cuda.Event()  # the tape is complete once the recording launch is
         ctx.recorded.record(torch.cuda.current_stream(x0c.device))
-        ctx.fwd_stream = torch.cuda.current_stream(x0c.device).cuda_stream
         return x, status
 
     @staticmethod
@@ -133,17 +125,9 @@ class _FusedSolve(torch.autograd.Function):
             return (None,) * 8
         # autograd may run this backward on another stream than the recording launch's: order the
         # adjoint after the tape is written
-        cur = torch.cuda.current_stream(tape.device)
-        if os.environ.get("DAVA_DEBUG_STREAMS"):
-            print(f"[dava] adjoint stream {cur.cuda_stream:#x}, recording stream {ctx.fwd_stream:#x}", flush=True)
-        if not os.environ.get("DAVA_NO_ADJOINT_WAIT"):
-            cur.wait_event(ctx.recorded)
-        if os.environ.get("DAVA_SYNC_BEFORE_BACKWARD"):  # diagnostic
-            torch.cuda.synchronize(tape.device)
+        torch.cuda.current_stream(tape.device).wait_event(ctx.recorded)
         gx, gobs = torch.ops.dava.ba_solve_backward(_c(x_grad.to(torch.float32)), tape, status, obs, vis, m, n, dist,
                                                     iters, residual, bool(need_obs))
-        if os.environ.get("DAVA_SYNC_AFTER_BACKWARD"):  # diagnostic
-            torch.cuda.synchronize(tape.device)
         return (gx if need_x else None, gobs if need_obs else None, None, None, None, None, None, None)
 
 

@@ -114,11 +114,11 @@ def _check_k100(out, ref, x0, obs, vis, m, n, distortion, env, env_intrinsics=No
         _report(tag, rel, env, {"n_objective_fallback": int(outside.sum())})
     # every problem within its envelope, or (a near-tie branch at fp32 stagnation) at the same objective
     assert (~outside | same_objective).all(), (rel.tolist(), env.tolist(), e_gpu.tolist(), e_ref.tolist())
-    # ... and the objective fallback is the exception: at most 1 problem in 8
-    assert int(outside.sum()) <= max(1, rel.numel() // 8), (rel.tolist(), env.tolist())
+    # ... and the objective fallback is the exception: at most one problem per case
+    assert int(outside.sum()) <= 1, (rel.tolist(), env.tolist())
     if env_intrinsics is not None:
         assert ((_rel(out[:, :3], ref[:, :3]) <= env_intrinsics) | same_objective).all()
-    assert (rel <= TOL).double().mean() >= 0.75, rel
+    assert (rel <= TOL).double().mean() >= 0.9, rel
 
 
 @pytest.mark.parametrize("mode", ["dense", "compact"])

@@ -32,11 +32,7 @@ def main():
             except Exception:
                 pass
         out, gx, go, st = T._fused_grads(dev, x0, obs, vis, m, n, False, w, ray, **kw)
-        from deep_attention_visual_odometry_amd import native_ops
-        tape = native_ops.LAST_TAPE.cpu().view(torch.float32) if native_ops.LAST_TAPE is not None else None
         cur = (out, gx, go)
-        if first is None:
-            first_tape = tape
         if first is None:
             first = cur
             continue
@@ -44,13 +40,8 @@ def main():
         if d:
             bad += 1
             rows = (first[1] != cur[1]).any(-1).nonzero().flatten().tolist()
-            where = []
-            if tape is not None:
-                diff = (tape != first_tape) & ~(torch.isnan(tape) & torch.isnan(first_tape))
-                where = diff.nonzero().flatten().tolist()
             print(f"run {r}: differs in {d}, gradient rows {rows}, "
-                  f"max rel {(T._rows_rel(cur[1], first[1])).max().item():.3e}, tape float offsets {where[:12]} "
-                  f"({len(where)})", flush=True)
+                  f"max rel {(T._rows_rel(cur[1], first[1])).max().item():.3e}", flush=True)
     print(f"{bad} of {runs - 1} repeats differ", flush=True)
 
 
