@@ -51,6 +51,10 @@ struct AdjointArgs {
 };
 
 constexpr int kAdjWaves = 4;
+#ifndef DAVA_ADJ_INFLIGHT
+#define DAVA_ADJ_INFLIGHT 2  // 4 and 8 measured no faster / 10% slower at C3
+#endif
+constexpr int kAdjInflight = DAVA_ADJ_INFLIGHT;  // entries per wave in flight in the passes
 constexpr int kAdjBlock = kWave * kAdjWaves;
 
 struct AdjointCarve {
@@ -135,13 +139,15 @@ __device__ __forceinline__ void pair_pass(int P, int Pv, int j0, int j1, const f
       pb[m] += k3 * r1[m] + k4 * r2[m];
     }
   };
+  // EF entries of this wave in flight: at one wave per SIMD (the dual evaluation needs > 256
+  // registers) the streams are latency-bound, and the register file has room for the rows
   int j = j0 + wave;
-  for (; j + kAdjWaves < j1; j += 2 * kAdjWaves) {
-    f4a r1a[GM], r2a[GM], r1b[GM], r2b[GM];
-    load(j, r1a, r2a);
-    load(j + kAdjWaves, r1b, r2b);
-    consume(j, r1a, r2a);
-    consume(j + kAdjWaves, r1b, r2b);
+  for (; j + (kAdjInflight - 1) * kAdjWaves < j1; j += kAdjInflight * kAdjWaves) {
+    f4a r1[kAdjInflight][GM], r2[kAdjInflight][GM];
+#pragma unroll
+    for (int e = 0; e < kAdjInflight; ++e) load(j + e * kAdjWaves, r1[e], r2[e]);
+#pragma unroll
+    for (int e = 0; e < kAdjInflight; ++e) consume(j + e * kAdjWaves, r1[e], r2[e]);
   }
   for (; j < j1; j += kAdjWaves) {
     f4a r1[GM], r2[GM];
@@ -362,8 +368,10 @@ __global__ __launch_bounds__(kAdjBlock, 1) void bfgs_ba_adjoint_kernel(AdjointAr
     }
     __syncthreads();
     Dual E(0.f), unused(0.f);
+#ifndef DAVA_ADJ_DIAG_NO_HVP  // timing-only diagnostic builds: skip the dual-number evaluation (wrong results)
     ba_eval<true, false, false, false, false, RES, Dual, kAdjWaves>(L, xd, nullptr, 0.f, obs, vis, gd, views, vpart,
                                                                    scratch, buf, E, unused, nullptr, obsacc);
+#endif
     for (int i = tid; i < P; i += kAdjBlock) xb[i] += gd[i].t;
     __syncthreads();
   }
