@@ -94,6 +94,8 @@ for _t in ("f32", "f64"):
         f"dava_bfgs_update_inverse_hessian_backward_{_t}": (ctypes.c_int, [_c_i64, _c_i64] + [_vp] * 8),
         f"dava_l1_camera_evaluate_{_t}": (ctypes.c_int, [_c_i64, _c_i32, _c_i32, _c_i32] + [_vp] * 8
                                           + [_scalar] * 4 + [_vp, _vp, _vp]),
+        f"dava_l1_camera_vjp_{_t}": (ctypes.c_int, [_c_i64, _c_i32, _c_i32, _c_i32] + [_vp] * 8 + [_scalar] * 4
+                                     + [_vp, _vp, _c_i32, _vp, _vp]),
         f"dava_bfgs_initial_scale_backward_{_t}": (ctypes.c_int, [_c_i64, _c_i64] + [_vp] * 6),
         f"dava_bfgs_scale_matrix_backward_{_t}": (ctypes.c_int, [_c_i64, _c_i64] + [_vp] * 6),
         f"dava_bfgs_search_direction_backward_{_t}": (ctypes.c_int, [_c_i64, _c_i64] + [_vp] * 6),

@@ -524,7 +524,49 @@ def _(focal, cx, cy, translation, lie, world, target, visibility, minimum_z_dist
             focal.new_empty((b, e, 3 + 6 * m + 3 * n - 7) if want_gradient else (0,)))
 
 
+@torch.library.custom_op("dava::l1_camera_vjp", mutates_args=(), device_types=_CUDA)
+def l1_camera_vjp(focal: Tensor, cx: Tensor, cy: Tensor, translation: Tensor, lie: Tensor, world: Tensor,
+                  target: Tensor, visibility: Tensor, minimum_z_distance: float, maximum_pixel_ratio: float,
+                  max_gradient: float, error_scale: float, error_cotangent: Optional[Tensor],
+                  gradient_cotangent: Optional[Tensor], detach_points: bool) -> Tensor:
+    """``dava_l1_camera_vjp``: the model's inputs' cotangent (B, E, D), D = 3 + 6M + 3(N-2) in the
+    order focal, cx, cy, translation (M, 3), lie (M, 3), world (N-2, 3), from the error's (B, E)
+    and / or the gradient's (B, E, P) cotangents.  Same input shapes as ``l1_camera_evaluate``."""
+    b, e = focal.shape
+    m, n = target.shape[1], target.shape[2]
+    p = 3 + 6 * m + 3 * n - 7
+    for t, shape, what in ((cx, (b, e), "cx"), (cy, (b, e), "cy"), (translation, (b, e, m, 3), "translation"),
+                           (lie, (b, e, m, 3), "orientation"), (world, (b, e, n - 2, 3), "world_points"),
+                           (target, (b, m, n, 2), "true_projected_points")):
+        _same(t, focal, shape, what)
+    if error_cotangent is not None:
+        _same(error_cotangent, focal, (b, e), "error cotangent")
+    if gradient_cotangent is not None:
+        _same(gradient_cotangent, focal, (b, e, p), "gradient cotangent")
+    if tuple(visibility.shape) != (b, m, n) or visibility.dtype != torch.uint8 or not visibility.is_contiguous():
+        raise ValueError("visibility must be a contiguous (B, M, N) uint8 tensor")
+    out = focal.new_zeros((b, e, 3 + 6 * m + 3 * (n - 2)))
+    if error_cotangent is None and gradient_cotangent is None:
+        return out
+    with torch.cuda.device(focal.device):
+        N.check(getattr(N.load_library(), f"dava_l1_camera_vjp_{_dt(focal)}")(
+            b, e, m, n, N.ptr(focal), N.ptr(cx), N.ptr(cy), N.ptr(translation), N.ptr(lie), N.ptr(world),
+            N.ptr(target), N.ptr(visibility), minimum_z_distance, maximum_pixel_ratio, max_gradient, error_scale,
+            N.ptr(error_cotangent) if error_cotangent is not None else None,
+            N.ptr(gradient_cotangent) if gradient_cotangent is not None else None, int(detach_points), N.ptr(out),
+            N.stream_of(focal.device)), "dava_l1_camera_vjp")
+    return out
+
+
+@l1_camera_vjp.register_fake
+def _(focal, cx, cy, translation, lie, world, target, visibility, minimum_z_distance, maximum_pixel_ratio,
+      max_gradient, error_scale, error_cotangent, gradient_cotangent, detach_points):
+    b, e = focal.shape
+    m, n = target.shape[1], target.shape[2]
+    return focal.new_empty((b, e, 3 + 6 * m + 3 * (n - 2)))
+
+
 OPS = ("ba_solve", "ba_solve_record", "ba_solve_backward", "ba_evaluate", "ba_second_order", "bfgs_update_inverse_hessian",
        "bfgs_update_inverse_hessian_backward", "bfgs_initial_scale", "bfgs_initial_scale_backward",
        "bfgs_scale_matrix", "bfgs_scale_matrix_backward", "bfgs_search_direction", "bfgs_search_direction_backward",
-       "wolfe_init", "wolfe_propose", "wolfe_update", "l1_camera_evaluate")
+       "wolfe_init", "wolfe_propose", "wolfe_update", "l1_camera_evaluate", "l1_camera_vjp")

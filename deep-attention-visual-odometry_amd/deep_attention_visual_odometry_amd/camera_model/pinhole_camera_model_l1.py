@@ -10,10 +10,14 @@ reference's L1 error and its HAND-WRITTEN gradient (max_gradient clipping includ
 ``as_parameters_vector`` returns the (B, E, P) vector ``add`` consumes (the reference's
 cannot run for its own tensor shapes, see the method).
 
-Autograd through the model's error/gradient tensors (the reference's
-``enable_error_gradients`` / ``enable_grad_gradients``) is not provided: if an input
-tensor requires grad while grad mode is on, evaluation raises instead of silently
-returning a detached value.
+Autograd through the model's error/gradient tensors follows the reference's
+``enable_error_gradients`` / ``enable_grad_gradients`` (``:139-198``): the backward is the
+HIP VJP kernel (``dava_l1_camera_vjp``: one forward-mode dual-number pass per input element,
+contracted with the cotangents in-kernel).  With ``enable_error_gradients=False`` the error is
+returned detached; with ``enable_grad_gradients=False`` the gradient is differentiated with the
+world and camera-relative points held constant, as the reference's detaches do.  Gradients
+into ``true_projected_points`` are not provided: if it requires grad under grad mode,
+evaluation raises.
 """
 from typing import Optional
 
@@ -28,6 +32,40 @@ from ..utils import merge_cached_values
 
 def _c(t: torch.Tensor) -> torch.Tensor:
     return t if t.is_contiguous() else t.contiguous()
+
+
+class _L1Evaluate(torch.autograd.Function):
+    """error (B, E) / gradient (B, E, P) of the six parameter tensors, differentiable: the backward
+    is ``dava::l1_camera_vjp`` (two launches when the gradient's points are detached and the
+    error's are not)."""
+
+    @staticmethod
+    def forward(ctx, fixed, want_error, want_gradient, focal, cx, cy, trans, lie, world):
+        target, vis, min_z, ratio, mg, scale, detach_points = fixed
+        err, grad = torch.ops.dava.l1_camera_evaluate(focal, cx, cy, trans, lie, world, target, vis, min_z, ratio,
+                                                      mg, scale, want_error, want_gradient)
+        ctx.save_for_backward(focal, cx, cy, trans, lie, world)
+        ctx.fixed, ctx.want = fixed, (want_error, want_gradient)
+        return err, grad
+
+    @staticmethod
+    @torch.autograd.function.once_differentiable
+    def backward(ctx, g_err, g_grad):
+        focal, cx, cy, trans, lie, world = ctx.saved_tensors
+        target, vis, min_z, ratio, mg, scale, detach_points = ctx.fixed
+        ge = _c(g_err) if (g_err is not None and ctx.want[0]) else None
+        gg = _c(g_grad) if (g_grad is not None and ctx.want[1]) else None
+        args = (focal, cx, cy, trans, lie, world, target, vis, min_z, ratio, mg, scale)
+        if detach_points and ge is not None and gg is not None:
+            vjp = torch.ops.dava.l1_camera_vjp(*args, ge, None, False) + torch.ops.dava.l1_camera_vjp(
+                *args, None, gg, True)
+        else:
+            vjp = torch.ops.dava.l1_camera_vjp(*args, ge, gg, bool(detach_points and gg is not None))
+        b, e, m = trans.shape[0], trans.shape[1], trans.shape[2]
+        n2 = world.shape[2]
+        d_f, d_cx, d_cy, d_t, d_l, d_w = torch.split(vjp, [1, 1, 1, 3 * m, 3 * m, 3 * n2], dim=-1)
+        return (None, None, None, d_f.reshape(b, e), d_cx.reshape(b, e), d_cy.reshape(b, e), d_t.reshape(b, e, m, 3),
+                d_l.reshape(b, e, m, 3), d_w.reshape(b, e, n2, 3))
 
 
 class PinholeCameraModelL1(IOptimisableFunction):
@@ -118,10 +156,11 @@ class PinholeCameraModelL1(IOptimisableFunction):
         N.require_device_tensor(self._focal_length, "focal_length")
         inputs = (self._focal_length, self._cx, self._cy, self._translation, self._orientation.lie_vector,
                   self._world_points)
-        if torch.is_grad_enabled() and any(t.requires_grad for t in inputs + (self._true_projected_points,)):
+        differentiable = torch.is_grad_enabled() and any(t.requires_grad for t in inputs)
+        if torch.is_grad_enabled() and self._true_projected_points.requires_grad:
             raise NotImplementedError(
-                "autograd through PinholeCameraModelL1's error/gradient is not implemented on the GPU path; "
-                "evaluate under torch.no_grad() or detach the model's tensors")
+                "gradients into PinholeCameraModelL1's true_projected_points are not implemented on the GPU path; "
+                "detach them (the parameters may require grad)")
         dt = self._focal_length.dtype
         for t in inputs[1:] + (self._true_projected_points,):
             dt = torch.promote_types(dt, t.dtype)  # the dtype the reference's expressions produce
@@ -131,19 +170,26 @@ class PinholeCameraModelL1(IOptimisableFunction):
             raise TypeError("PinholeCameraModelL1 evaluates in float32 or float64")
         b, e, m, n = self.batch_size, self.num_estimates, self._num_views, self._num_points
         dev = self.device
-        cast = lambda t: _c(t.detach().to(device=dev, dtype=dt))  # noqa: E731
+        cast = lambda t: _c(t.to(device=dev, dtype=dt))  # noqa: E731  (differentiable when needed)
         focal = cast(self._focal_length).reshape(b, e)
         cx = cast(self._cx).reshape(b, e)
         cy = cast(self._cy).reshape(b, e)
         trans = cast(self._translation).reshape(b, e, m, 3)
         lie = cast(self._orientation.lie_vector).reshape(b, e, m, 3)
         world = cast(self._world_points).reshape(b, e, n - 2, 3)
-        target = cast(self._true_projected_points).reshape(b, m, n, 2)
+        target = cast(self._true_projected_points.detach()).reshape(b, m, n, 2)
         vis = _c(self._visibility_mask.detach().to(device=dev, dtype=torch.uint8)).reshape(b, m, n)
-        err, grad = torch.ops.dava.l1_camera_evaluate(
-            focal, cx, cy, trans, lie, world, target, vis, float(self.minimum_z_distance),
-            float(self.maximum_pixel_ratio), float(self._max_gradient), float(self._error_scale.item()),
-            bool(want_error), bool(want_gradient))
+        fixed = (target, vis, float(self.minimum_z_distance), float(self.maximum_pixel_ratio),
+                 float(self._max_gradient), float(self._error_scale.item()), not self._enable_grad_gradients)
+        if differentiable:
+            err, grad = _L1Evaluate.apply(fixed, bool(want_error), bool(want_gradient), focal, cx, cy, trans, lie,
+                                          world)
+            if not self._enable_error_gradients:
+                err = err.detach()  # the reference detaches u, v (:139-141)
+        else:
+            err, grad = torch.ops.dava.l1_camera_evaluate(focal.detach(), cx.detach(), cy.detach(), trans.detach(),
+                                                          lie.detach(), world.detach(), *fixed[:6],
+                                                          bool(want_error), bool(want_gradient))
         err = err if want_error else None
         grad = grad if want_gradient else None
         return err, grad

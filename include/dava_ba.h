@@ -290,6 +290,30 @@ int dava_l1_camera_evaluate_f64(int64_t batch, int32_t estimates, int32_t views,
                                 double max_gradient, double error_scale, double* error_out, double* gradient_out,
                                 void* stream);
 
+/* Reverse mode through the model above (the reference's autograd through get_error /
+ * get_gradient when enable_error_gradients / enable_grad_gradients allow it,
+ * pinhole_camera_model_l1.py:132-285).  For every estimate and every input element
+ * d in [0, D), D = 3 + 6 views + 3 (points-2), ordered focal, cx, cy, translation (views, 3),
+ * lie_vector (views, 3), world_points (points-2, 3):
+ *   input_cotangent_out[b, e, d] = error_cotangent[b, e] d error/d x_d
+ *                                + sum_q gradient_cotangent[b, e, q] d gradient_q/d x_d
+ * (either cotangent may be NULL).  detach_points != 0 differentiates the gradient with the world
+ * and camera-relative points held constant, as the reference's enable_grad_gradients = False
+ * does (:185-198).  Branches, clamps and clips take the derivative of the branch taken;
+ * sign() is flat.  One workgroup per (b, e, d); deterministic.                              */
+int dava_l1_camera_vjp_f32(int64_t batch, int32_t estimates, int32_t views, int32_t points, const float* focal,
+                           const float* cx, const float* cy, const float* translation, const float* lie_vector,
+                           const float* world_points, const float* true_points, const uint8_t* visibility,
+                           float minimum_z_distance, float inverse_pixel_ratio, float max_gradient, float error_scale,
+                           const float* error_cotangent, const float* gradient_cotangent, int32_t detach_points,
+                           float* input_cotangent_out, void* stream);
+int dava_l1_camera_vjp_f64(int64_t batch, int32_t estimates, int32_t views, int32_t points, const double* focal,
+                           const double* cx, const double* cy, const double* translation, const double* lie_vector,
+                           const double* world_points, const double* true_points, const uint8_t* visibility,
+                           double minimum_z_distance, double inverse_pixel_ratio, double max_gradient,
+                           double error_scale, const double* error_cotangent, const double* gradient_cotangent,
+                           int32_t detach_points, double* input_cotangent_out, void* stream);
+
 /* ---- misc ---- */
 const char* dava_status_string(int status);
 int dava_abi_version(void);

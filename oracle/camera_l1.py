@@ -15,9 +15,7 @@ import torch
 from .trig import sinc, sinc_slope, versine_ratio
 
 
-def _d_term(x: torch.Tensor) -> torch.Tensor:
-    """sin x / x^3 - 2 (1 - cos x) / x^4, series below 0.25
-    (``utils/func_sin_x_on_x_cubed_minus_two_one_minus_cos_x_on_x_fourth.py:8-40``)."""
+def _d_term_value(x: torch.Tensor) -> torch.Tensor:
     near = torch.less(x.abs(), 0.25)
     far = torch.logical_not(near)
     out = torch.empty_like(x)
@@ -30,6 +28,31 @@ def _d_term(x: torch.Tensor) -> torch.Tensor:
     x3 = x[far] * x2[far]
     out[far] = s / x3 - 2.0 * (1.0 - c) / x4[far]
     return out
+
+
+class _DTerm(torch.autograd.Function):
+    """``SinXonXCubedMinusTwoOneMinusCosXonXFourth`` (:6-58): backward grad (C(x) - 4 D(x)) / x,
+    1/x taken as 0 at 0."""
+
+    @staticmethod
+    def forward(ctx, x):
+        out = _d_term_value(x)
+        ctx.save_for_backward(x, out)
+        return out
+
+    @staticmethod
+    def backward(ctx, grad):
+        x, out = ctx.saved_tensors
+        recip = 1 / x
+        recip[x == 0] = 0.0
+        return grad * recip * (sinc_slope(x) - 4.0 * out)
+
+
+def _d_term(x: torch.Tensor) -> torch.Tensor:
+    """sin x / x^3 - 2 (1 - cos x) / x^4, series below 0.25
+    (``utils/func_sin_x_on_x_cubed_minus_two_one_minus_cos_x_on_x_fourth.py:8-40``), with the
+    reference's backward."""
+    return _DTerm.apply(x)
 
 
 def world_points(world: torch.Tensor) -> torch.Tensor:
@@ -115,12 +138,16 @@ def l1_error(focal, cx, cy, translation, lie, world, true, vis, minimum_z_distan
 
 
 def l1_gradient(focal, cx, cy, translation, lie, world, true, vis, minimum_z_distance=1e-3, maximum_pixel_ratio=5.0,
-                max_gradient=-1.0):
+                max_gradient=-1.0, detach_points=False):
+    """``detach_points``: the reference's enable_grad_gradients = False, which detaches the world
+    points, the camera-relative points and u, v (``get_gradient`` :185-198) before the partials."""
     wp = world_points(world)
-    og = _parameter_gradient(lie, wp[:, :, None, :, :])
+    og = _parameter_gradient(lie, (wp.detach() if detach_points else wp)[:, :, None, :, :])
     rg = _vector_gradient(lie)
     p = camera_relative_points(translation, lie, world, minimum_z_distance, maximum_pixel_ratio)
     u, v = uv(focal, cx, cy, p)
+    if detach_points:
+        p, u, v = p.detach(), u.detach(), v.detach()
     scale = error_scale(true.size(1), true.size(2))
     ru = scale * vis[:, None, :, :] * (u - true[:, None, :, :, 0]).sign()
     rv = scale * vis[:, None, :, :] * (v - true[:, None, :, :, 1]).sign()
@@ -171,3 +198,27 @@ def l1_gradient(focal, cx, cy, translation, lie, world, true, vis, minimum_z_dis
     g_y = (ru[:, :, :, 2:] * du_dy[:, :, :, 2:] + rv[:, :, :, 2:] * dv_dy[:, :, :, 2:]).sum(dim=-2)
     g_z = (ru[:, :, :, 3:] * du_dz[:, :, :, 3:] + rv[:, :, :, 3:] * dv_dz[:, :, :, 3:]).sum(dim=-2)
     return torch.cat([g_cx, g_cy, g_f] + g_abc + [g_tx, g_ty, g_tz, g_x, g_y, g_z], dim=-1)
+
+
+PARAMETERS = ("focal_length", "cx", "cy", "translation", "lie", "world")
+
+
+def l1_autograd(parts, true, vis, enable_error_gradients=True, enable_grad_gradients=True, seed=5, weight_dtype=None,
+                **kw):
+    """d/d(parameters) of sum(we * error) + sum(wg * gradient) by autograd through the restatement,
+    the reference's enable_* detaches applied (``get_error`` :139-141, ``get_gradient`` :185-198);
+    weights from ``torch.Generator`` seed ``seed`` (drawn in ``weight_dtype``, default the
+    parts' dtype), the error's drawn first.  ``parts`` maps
+    PARAMETERS to tensors; returns the list of gradients in PARAMETERS order (zeros if unused)."""
+    leaves = {k: parts[k].clone().requires_grad_(True) for k in PARAMETERS}
+    args = [leaves[k] for k in PARAMETERS] + [true, vis]
+    zkw = {k: v for k, v in kw.items() if k != "max_gradient"}
+    err = l1_error(*args, **zkw)
+    grad = l1_gradient(*args, max_gradient=kw.get("max_gradient", -1.0), detach_points=not enable_grad_gradients,
+                       **zkw)
+    gen = torch.Generator().manual_seed(seed)
+    we = torch.randn(err.shape, generator=gen, dtype=weight_dtype or err.dtype).to(err.dtype)
+    wg = torch.randn(grad.shape, generator=gen, dtype=weight_dtype or grad.dtype).to(grad.dtype)
+    loss = (grad * wg).sum() + ((err * we).sum() if enable_error_gradients else 0.0)
+    out = torch.autograd.grad(loss, [leaves[k] for k in PARAMETERS], allow_unused=True)
+    return [o if o is not None else torch.zeros_like(leaves[k]) for o, k in zip(out, PARAMETERS)]

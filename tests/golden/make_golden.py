@@ -42,6 +42,8 @@ Fixtures written:
                           return_second_last, with ``torch.rand_like`` replaced by a seeded
                           CPU stream (``deterministic_rand_like``) so the run is
                           reproducible; the same replacement is applied in the parity tests.
+* ``camera_l1_autograd.npz`` -- autograd through that model's error / gradient for the
+                          enable_error_gradients / enable_grad_gradients settings.
 * ``camera_l1.npz``   -- the legacy IOptimisableFunction path: PinholeCameraModelL1
                           get_error / get_gradient (the hand-written gradient) for random
                           B x E x M x N models in fp64 and fp32 (max_gradient 1e3 and the
@@ -481,9 +483,49 @@ def gen_camera_l1():
     np.savez_compressed(os.path.join(HERE, "camera_l1.npz"), **out)
 
 
+def gen_camera_l1_autograd():
+    """Autograd THROUGH PinholeCameraModelL1.get_error / get_gradient (fp64): d/d(parameters) of
+    sum(we * error) + sum(wg * gradient) for the enable_error_gradients / enable_grad_gradients
+    settings, weights from torch.Generator seed 5 (error's drawn first)."""
+    out = {}
+    rng = np.random.default_rng(9400)
+    cases = {"mg1e3": dict(max_gradient=1e3), "default": dict(),
+             "behind": dict(max_gradient=50.0, minimum_z_distance=0.5)}
+    names = ("focal_length", "cx", "cy", "translation", "lie", "world")
+    for name, kw in cases.items():
+        _, parts, true, vis = _l1_model(rng, 3, 2, 4, 8, torch.float64, **kw)
+        if name == "behind":
+            parts["world"][1, :, 0:2, 2] = -9.0
+            parts["translation"][2, :, 1, 2] = 0.1
+        for k, v in parts.items():
+            out[f"{name}_{k}"] = v.numpy()
+        out[name + "_true"], out[name + "_vis"] = true.numpy(), vis.numpy()
+        for flags in ((True, True), (True, False), (False, True)):
+            from deep_attention_visual_odometry.camera_model import PinholeCameraModelL1
+            from deep_attention_visual_odometry.geometry.lie_rotation import LieRotation
+
+            leaves = {k: parts[k].clone().requires_grad_(True) for k in names}
+            model = PinholeCameraModelL1(
+                focal_length=leaves["focal_length"], cx=leaves["cx"], cy=leaves["cy"],
+                translation=leaves["translation"], orientation=LieRotation(leaves["lie"]),
+                world_points=leaves["world"], true_projected_points=true, visibility_mask=vis,
+                enable_error_gradients=flags[0], enable_grad_gradients=flags[1], **kw)
+            err, grad = model.get_error(), model.get_gradient()
+            gen = torch.Generator().manual_seed(5)
+            we = torch.randn(err.shape, generator=gen, dtype=err.dtype)
+            wg = torch.randn(grad.shape, generator=gen, dtype=grad.dtype)
+            loss = (grad * wg).sum() + ((err * we).sum() if err.requires_grad else 0.0)
+            got = torch.autograd.grad(loss, [leaves[k] for k in names], allow_unused=True)
+            tag = f"{name}_{int(flags[0])}{int(flags[1])}"
+            out[tag + "_error_requires_grad"] = np.array(err.requires_grad)
+            for k, g in zip(names, got):
+                out[f"{tag}_d_{k}"] = (g if g is not None else torch.zeros_like(leaves[k])).numpy()
+    np.savez_compressed(os.path.join(HERE, "camera_l1_autograd.npz"), **out)
+
+
 if __name__ == "__main__":
     torch.set_num_threads(8)
-    which = sys.argv[1:] or ["eval", "update", "ls", "traj", "ray", "grad", "train", "l1"]
+    which = sys.argv[1:] or ["eval", "update", "ls", "traj", "ray", "grad", "train", "l1", "l1grad"]
     if "eval" in which:
         gen_ba_eval()
     if "update" in which:
@@ -500,4 +542,6 @@ if __name__ == "__main__":
         gen_training()
     if "l1" in which:
         gen_camera_l1()
+    if "l1grad" in which:
+        gen_camera_l1_autograd()
     print("golden fixtures written to", HERE)

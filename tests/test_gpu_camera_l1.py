@@ -199,12 +199,111 @@ def test_legacy_bfgs_camera_solver_matches_reference(device):
     assert (out.get_error().cpu() < torch.tensor(g["solve_in_error"])).all()
 
 
-def test_autograd_through_the_model_is_refused_loudly(device):
+PARAMS = ("focal_length", "cx", "cy", "translation", "lie", "world")
+
+
+def _random_tensors(m, n, b=3, e=2, seed=0, dtype=torch.float64):
+    rng = np.random.default_rng(seed)
+    t = {
+        "focal_length": rng.uniform(0.5, 2.0, size=(b, e)),
+        "cx": rng.normal(0.0, 0.1, size=(b, e)),
+        "cy": rng.normal(0.0, 0.1, size=(b, e)),
+        "translation": rng.normal(0.0, 0.5, size=(b, e, m, 3)) + np.array([0.0, 0.0, 6.0]),
+        "lie": rng.normal(0.0, 0.4, size=(b, e, m, 1, 3)),
+        "world": rng.normal(0.0, 1.0, size=(b, e, n - 2, 3)),
+        "true": rng.normal(0.0, 0.3, size=(b, m, n, 2)),
+    }
+    t = {k: torch.tensor(v, dtype=dtype) for k, v in t.items()}
+    t["vis"] = torch.tensor(rng.random((b, m, n)) > 0.2)
+    return t
+
+
+def _autograd_grads(device, t, kw, enable_error, enable_grad, seed=5):
+    """d/d(params) of sum(we * error) + sum(wg * gradient) through the HIP model."""
+    leaves = {k: t[k].clone().to(device).requires_grad_(True) for k in PARAMS}
+    d = dict(t, **leaves)
+    model = _model(device, {k: d[k] for k in FIELDS}, enable_error_gradients=enable_error,
+                   enable_grad_gradients=enable_grad, **kw)
+    err, grad = model.get_error(), model.get_gradient()
+    gen = torch.Generator().manual_seed(seed)
+    we = torch.randn(err.shape, generator=gen, dtype=err.dtype).to(device)
+    wg = torch.randn(grad.shape, generator=gen, dtype=grad.dtype).to(device)
+    loss = (grad * wg).sum() + ((err * we).sum() if err.requires_grad else 0.0)
+    out = torch.autograd.grad(loss, [leaves[k] for k in PARAMS], allow_unused=True)
+    return err, [o if o is not None else torch.zeros_like(leaves[k]) for o, k in zip(out, PARAMS)]
+
+
+def _oracle_autograd_grads(t, kw, enable_error, enable_grad, seed=5):
+    parts = {k: t[k].double() for k in PARAMS}
+    return camera_l1.l1_autograd(parts, t["true"].double(), t["vis"], enable_error, enable_grad, seed=seed,
+                                 weight_dtype=t["focal_length"].dtype, **kw)
+
+
+AUTOGRAD_CASES = {
+    "mg20": (3, 5, dict(max_gradient=20.0, minimum_z_distance=0.01, maximum_pixel_ratio=3.0)),
+    "wide": (6, 70, dict(max_gradient=20.0, minimum_z_distance=0.01, maximum_pixel_ratio=3.0)),
+    "default": (3, 9, dict()),  # max_gradient -1: every partial clipped to a constant
+    "behind": (4, 12, dict(max_gradient=50.0, minimum_z_distance=6.0)),  # the z clamp is active
+}
+
+
+@pytest.mark.parametrize("case", list(AUTOGRAD_CASES))
+@pytest.mark.parametrize("flags", [(True, True), (True, False), (False, True)])
+def test_autograd_through_the_model_matches_oracle(device, case, flags):
+    """Autograd through get_error / get_gradient (the HIP VJP kernel) against autograd through the
+    oracle restatement, float64, for the reference's enable_error_gradients /
+    enable_grad_gradients settings (pinhole_camera_model_l1.py:132-285)."""
+    m, n, kw = AUTOGRAD_CASES[case]
+    t = _random_tensors(m, n, seed=m * 7 + n)
+    err, got = _autograd_grads(device, t, kw, *flags)
+    assert err.requires_grad == flags[0]
+    want = _oracle_autograd_grads(t, kw, *flags)
+    for k, a, b in zip(PARAMS, got, want):
+        scale = max(b.abs().max().item(), 1e-30)
+        assert (a.cpu().double() - b).abs().max().item() <= 1e-9 * scale + 1e-13, (case, flags, k)
+
+
+@pytest.mark.parametrize("case", ["mg1e3", "default", "behind"])
+@pytest.mark.parametrize("flags", ["11", "10", "01"])
+def test_autograd_through_the_model_matches_reference(device, case, flags):
+    """Against the REAL reference's autograd (tests/golden/camera_l1_autograd.npz), fp64."""
+    g = np.load(os.path.join(GOLDEN, "camera_l1_autograd.npz"))
+    kw = {"mg1e3": dict(max_gradient=1e3), "default": dict(),
+          "behind": dict(max_gradient=50.0, minimum_z_distance=0.5)}[case]
+    t = {k: torch.tensor(g[f"{case}_{k}"]) for k in FIELDS}
+    err, got = _autograd_grads(device, t, kw, flags[0] == "1", flags[1] == "1")
+    assert err.requires_grad == bool(g[f"{case}_{flags}_error_requires_grad"])
+    for k, a in zip(PARAMS, got):
+        want = torch.tensor(g[f"{case}_{flags}_d_{k}"])
+        scale = max(want.abs().max().item(), 1.0)
+        assert (a.cpu() - want).abs().max().item() <= 1e-9 * scale, (case, flags, k)
+
+
+def test_autograd_through_the_model_float32(device):
+    """float32 model, against the float64 oracle (fp32-rounded inputs)."""
+    m, n, kw = AUTOGRAD_CASES["mg20"]
+    t = _random_tensors(m, n, seed=11, dtype=torch.float32)
+    _, got = _autograd_grads(device, t, kw, True, True)
+    want = _oracle_autograd_grads(t, kw, True, True)
+    for k, a, b in zip(PARAMS, got, want):
+        assert a.dtype == torch.float32
+        assert _rel(a, b) < 1e-4, k
+
+
+def test_autograd_into_the_target_is_refused_loudly(device):
     g = np.load(os.path.join(GOLDEN, "camera_l1.npz"))
     t = {k: torch.tensor(g[f"default_f64_{k}"]) for k in FIELDS}
-    t["focal_length"] = t["focal_length"].requires_grad_(True)
+    t["true"] = t["true"].requires_grad_(True)
     with pytest.raises(NotImplementedError):
         _model(device, t).get_error()
+
+
+def test_no_grad_evaluation_of_a_differentiable_model_is_detached(device):
+    t = _random_tensors(3, 5)
+    t["focal_length"] = t["focal_length"].requires_grad_(True)
+    with torch.no_grad():
+        err = _model(device, t).get_error()
+    assert not err.requires_grad
 
 
 def test_parameters_vector_round_trips_through_add(device):

@@ -231,3 +231,22 @@ def test_gradient_through_fp32_solves_matches_reference_bitwise(name):
     assert np.array_equal(out.detach().numpy(), g[name + "_out"])
     assert np.array_equal(x0.grad.numpy(), g[name + "_grad"])
     assert np.array_equal(obs.grad.numpy(), g[name + "_obs_grad"])
+
+
+@pytest.mark.parametrize("case", ["mg1e3", "default", "behind"])
+@pytest.mark.parametrize("flags", ["11", "10", "01"])
+def test_camera_l1_autograd_matches_reference(case, flags):
+    """Autograd THROUGH PinholeCameraModelL1's error and hand-written gradient (second order),
+    with the enable_error_gradients / enable_grad_gradients detaches, fp64."""
+    from oracle import camera_l1
+
+    g = _load("camera_l1_autograd.npz")
+    kw = {"mg1e3": dict(max_gradient=1e3), "default": dict(), "behind": dict(max_gradient=50.0,
+                                                                             minimum_z_distance=0.5)}[case]
+    parts = {k: torch.tensor(g[f"{case}_{k}"]) for k in camera_l1.PARAMETERS}
+    got = camera_l1.l1_autograd(parts, torch.tensor(g[case + "_true"]), torch.tensor(g[case + "_vis"]),
+                                flags[0] == "1", flags[1] == "1", **kw)
+    assert bool(g[f"{case}_{flags}_error_requires_grad"]) == (flags[0] == "1")
+    for k, a in zip(camera_l1.PARAMETERS, got):
+        want = g[f"{case}_{flags}_d_{k}"]
+        assert np.allclose(a.numpy(), want, rtol=1e-10, atol=1e-12 * max(np.abs(want).max(), 1.0)), k
