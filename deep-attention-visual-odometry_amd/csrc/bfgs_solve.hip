@@ -621,6 +621,13 @@ __device__ __forceinline__ float wide_direction(int P, int Pv, int nh, const flo
 #ifndef DAVA_FUSED_INFLIGHT_LARGE
 #define DAVA_FUSED_INFLIGHT_LARGE 2  // 3-4 groups per lane (P <= 1024; C3)
 #endif
+// Ring (1): refill each entry slot as soon as it is consumed, so loads overlap the batch's
+// arithmetic.  Rejected: the kernel is at the 256-VGPR cap, the refills keep the slots live
+// through every consume, and the spills (scratch ops 26 -> 201) cost C3 -33 %, C2 -13 %
+// (interleaved A/B, bitwise equal, profiles/r02_ab_history_ring.log).
+#ifndef DAVA_HISTORY_RING
+#define DAVA_HISTORY_RING 0  // 0: load a batch of EF entries, consume it, then load the next
+#endif
 template <int GM>
 __host__ __device__ constexpr int fused_inflight() {
   return DAVA_FUSED_PAIR ? (GM <= 2 ? DAVA_FUSED_INFLIGHT_SMALL : DAVA_FUSED_INFLIGHT_LARGE) : 1;
@@ -728,6 +735,26 @@ __device__ __forceinline__ void compact_products_fused(int P, int Pv, int nh, co
     consume(j, s0, w0);
   }
   if constexpr (EF > 1) {  // EF entries of this wave in flight: all loads issued before any is consumed
+#if DAVA_HISTORY_RING
+    // ring: each register slot is refilled with the entry EF * NW ahead as soon as it has been
+    // consumed, so the next entries' loads are in flight while this batch is consumed (the batch
+    // form waits out a full load latency per batch).  Same entries, same order: bitwise equal.
+    if (j + (EF - 1) * NW < nh) {
+      f4v s[EF][GM], w[EF][GM];
+#pragma unroll
+      for (int e = 0; e < EF; ++e) load(j + e * NW, s[e], w[e]);
+      for (; j + (2 * EF - 1) * NW < nh; j += EF * NW) {
+#pragma unroll
+        for (int e = 0; e < EF; ++e) {
+          consume(j + e * NW, s[e], w[e]);
+          load(j + (EF + e) * NW, s[e], w[e]);
+        }
+      }
+#pragma unroll
+      for (int e = 0; e < EF; ++e) consume(j + e * NW, s[e], w[e]);
+      j += EF * NW;
+    }
+#else
     for (; j + (EF - 1) * NW < nh; j += EF * NW) {
       f4v s[EF][GM], w[EF][GM];
 #pragma unroll
@@ -735,6 +762,7 @@ __device__ __forceinline__ void compact_products_fused(int P, int Pv, int nh, co
 #pragma unroll
       for (int e = 0; e < EF; ++e) consume(j + e * NW, s[e], w[e]);
     }
+#endif
   }
   for (; j < nh; j += NW) {  // the rest, one entry in flight
     f4v s0[GM], w0[GM];
