@@ -1594,7 +1594,16 @@ static int solve_impl(const DavaScene* scene, const DavaSolverConfig* config, co
     a.tape_s = t + tl.scal;
   }
   hipStream_t s = static_cast<hipStream_t>(stream);
-  if (queue && hipMemsetAsync(a.queue, 0, sizeof(int), s) != hipSuccess) return DAVA_ERR_LAUNCH;
+  // (a recording zeroes its whole queue tail: the tape tensor handed back includes it)
+  if (record && workspace_bytes >= need + kQueueBytes) {
+    if (hipMemsetAsync(static_cast<char*>(workspace) + need, 0, kQueueBytes, s) != hipSuccess) return DAVA_ERR_LAUNCH;
+  } else if (queue && hipMemsetAsync(a.queue, 0, sizeof(int), s) != hipSuccess) {
+    return DAVA_ERR_LAUNCH;
+  }
+  // the tape's scalar rows have slots no solve writes (rho / c of step K, padding): zero them so a
+  // tape is a deterministic function of the inputs, byte for byte (B x T floats, small)
+  if (record && hipMemsetAsync(a.tape_s, 0, (size_t)scene->batch * tl.T * sizeof(float), s) != hipSuccess)
+    return DAVA_ERR_LAUNCH;
 #if DAVA_PHASE_TIMING
   const size_t ph_bytes = (size_t)scene->batch * kPhases * sizeof(unsigned long long);
   if (hipMalloc(&a.phase_cycles, ph_bytes) != hipSuccess) return DAVA_ERR_LAUNCH;

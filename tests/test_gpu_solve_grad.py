@@ -355,6 +355,23 @@ def test_recording_solve_is_bitwise_the_solve(device):
     assert torch.equal(x, xr) and torch.equal(st, str_)
 
 
+def test_recording_tape_is_deterministic(device):
+    """Two recordings of the same solve give byte-identical tapes, whatever the memory held before
+    (the slots no solve writes are zeroed)."""
+    from deep_attention_visual_odometry_amd import make_scenes
+
+    s = make_scenes(8, 2, 64, distortion=False, seed=934, drop=0.1)
+    x0, obs, vis = (torch.tensor(t).to(device) for t in (s.initial, s.observations, s.visibility))
+    vis = vis.to(torch.uint8)
+    args = (x0, obs, vis, 2, 64, False, 1e-4, 0.9, -1.0, 10, -1.0, 1000, True, 0)
+    _, _, tape = torch.ops.dava.ba_solve_record(*args)
+    first = tape.clone()
+    junk = torch.empty_like(tape).fill_(255)  # the next tape's allocation starts as 0xFF bytes
+    del tape, junk
+    _, _, tape = torch.ops.dava.ba_solve_record(*args)
+    assert torch.equal(tape, first)
+
+
 def test_fused_and_generic_backward_agree_c3(device, monkeypatch):
     """C3 + Brown-Conrady, K = 30: the adjoint kernel and the generic loop (dense H per iteration in
     torch's graph, HIP VJP kernels) give the same gradients."""
