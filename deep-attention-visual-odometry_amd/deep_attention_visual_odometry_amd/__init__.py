@@ -8,6 +8,7 @@ Drop-in for the hot path of jskinn/deep-attention-visual-odometry
 from .autograd_solvers import BFGSSolver, line_search_wolfe_conditions
 from .camera_model import RayAngleError, ReprojectionError, num_parameters, unpack_calibration_parameters
 from .camera_model import PinholeCameraModelL1
+from .data import CameraAndParametersDataset, CameraViewsAndPoints
 from .geometry import LieRotation
 from .scenes import make_scenes
 from .solvers import BFGSCameraSolver, IOptimisableFunction, LineSearchStrongWolfeConditions
@@ -20,6 +21,8 @@ __all__ = [
     "num_parameters",
     "unpack_calibration_parameters",
     "make_scenes",
+    "CameraAndParametersDataset",
+    "CameraViewsAndPoints",
     # legacy IOptimisableFunction path (solvers/, camera_model/pinhole_camera_model_l1.py)
     "BFGSCameraSolver",
     "IOptimisableFunction",

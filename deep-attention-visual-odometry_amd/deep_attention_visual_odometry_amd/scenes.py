@@ -126,8 +126,6 @@ def make_scenes(
         raise ValueError("num_views must be >= 2 (the scale normalisation needs a translation)")
     if ray_angle and distortion:
         raise ValueError("the ray-angle objective is pinhole only")
-    if num_views < 2:
-        raise ValueError("num_views must be >= 2 (the scale normalisation needs a translation)")
     p = parameter_count(num_views, num_points, distortion)
     truth = np.empty((batch, p))
     initial = np.empty((batch, p), dtype=np.float32)
