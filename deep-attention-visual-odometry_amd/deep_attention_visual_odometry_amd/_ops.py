@@ -115,6 +115,27 @@ def _(x0, observations, visibility, num_views, num_points, distortion, sufficien
             x0.new_empty((b, N.STATUS_WORDS), dtype=torch.int32))
 
 
+@torch.library.custom_op("dava::bfgs_solve", mutates_args=(), device_types=_CUDA)
+def bfgs_solve(parameters: Tensor, observations: Tensor, visibility: Tensor, num_views: int, num_points: int,
+               distortion: bool = False, iterations: int = 1000, error_threshold: float = 1e-4,
+               minimum_step: float = 1e-8, sufficient_decrease: float = 1e-4, curvature: float = 0.9,
+               residual: int = 0) -> Tuple[Tensor, Tensor]:
+    """The functional entry SURVEY.md 8(b) names: ``BFGSSolver().eval()`` on the fused objective with
+    the reference's defaults (``bfgs_solver.py:49-60``, strong Wolfe, ``wolfe_conditions.py:116``'s
+    1000 trials), compact inverse-Hessian history, workspace allocated per call.
+    Returns (x (B, P), status (B, 4) int32: steps, stop reason, evaluations, line-search trials)."""
+    x, _, status = ba_solve(parameters, observations, visibility, num_views, num_points, distortion,
+                            sufficient_decrease, curvature, error_threshold, iterations, minimum_step, 1000, True,
+                            N.DAVA_HESSIAN_COMPACT, residual, False, _empty0(parameters, torch.uint8))
+    return x, status
+
+
+@bfgs_solve.register_fake
+def _(parameters, observations, visibility, num_views, num_points, distortion=False, iterations=1000,
+      error_threshold=1e-4, minimum_step=1e-8, sufficient_decrease=1e-4, curvature=0.9, residual=0):
+    return torch.empty_like(parameters), parameters.new_empty((parameters.shape[0], N.STATUS_WORDS), dtype=torch.int32)
+
+
 @torch.library.custom_op("dava::ba_evaluate", mutates_args=(), device_types=_CUDA)
 def ba_evaluate(x: Tensor, observations: Tensor, visibility: Tensor, num_views: int, num_points: int,
                 distortion: bool, direction: Optional[Tensor], alpha: Optional[Tensor], want_grad: bool,
@@ -566,7 +587,7 @@ def _(focal, cx, cy, translation, lie, world, target, visibility, minimum_z_dist
     return focal.new_empty((b, e, 3 + 6 * m + 3 * (n - 2)))
 
 
-OPS = ("ba_solve", "ba_solve_record", "ba_solve_backward", "ba_evaluate", "ba_second_order", "bfgs_update_inverse_hessian",
+OPS = ("bfgs_solve", "ba_solve", "ba_solve_record", "ba_solve_backward", "ba_evaluate", "ba_second_order", "bfgs_update_inverse_hessian",
        "bfgs_update_inverse_hessian_backward", "bfgs_initial_scale", "bfgs_initial_scale_backward",
        "bfgs_scale_matrix", "bfgs_scale_matrix_backward", "bfgs_search_direction", "bfgs_search_direction_backward",
        "wolfe_init", "wolfe_propose", "wolfe_update", "l1_camera_evaluate", "l1_camera_vjp")

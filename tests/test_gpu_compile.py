@@ -119,6 +119,7 @@ def _op_samples(device):
     out = [
         (torch.ops.dava.ba_solve.default, (x, obs, vis, 2, 16, False, 1e-4, 0.9, -1.0, 5, -1.0, 1000, True,
                                            N.DAVA_HESSIAN_COMPACT, 0, True, ws)),
+        (torch.ops.dava.bfgs_solve.default, (x, obs, vis, 2, 16, False, 5, -1.0, -1.0)),
         (torch.ops.dava.ba_evaluate.default, (x, obs, vis, 2, 16, False, d, al, True, True, 0)),
         (torch.ops.dava.ba_evaluate.default, (x, obs, vis, 2, 16, False, None, None, False, False, 0)),
         (torch.ops.dava.ba_second_order.default, (x, obs, vis, 2, 16, False, d, 0, True, True)),
@@ -143,7 +144,38 @@ def _op_samples(device):
             (torch.ops.dava.bfgs_search_direction_backward.default, (h, sv, yv, True, True)),
             (torch.ops.dava.wolfe_init.default, (-sv, sc, sv)),
         ]
+    for dt in (torch.float32, torch.float64):  # the legacy camera model and its VJP
+        t = lambda *shape: torch.randn(*shape, generator=g, dtype=dt).to(device)  # noqa: E731
+        f = (t(2, 3).abs() + 0.5, t(2, 3) * 0.1, t(2, 3) * 0.1)
+        tr = t(2, 3, 4, 3) * 0.3 + torch.tensor([0.0, 0.0, 6.0], dtype=dt, device=device)
+        lie, world, target = t(2, 3, 4, 3) * 0.3, t(2, 3, 6, 3), t(2, 4, 8, 2) * 0.3
+        v8 = (torch.rand(2, 4, 8, generator=g) > 0.2).to(torch.uint8).to(device)
+        args = f + (tr, lie, world, target, v8, 0.01, 1 / 3.0, 20.0, 0.25)
+        out += [
+            (torch.ops.dava.l1_camera_evaluate.default, args + (True, True)),
+            (torch.ops.dava.l1_camera_vjp.default, args + (t(2, 3), t(2, 3, 3 + 6 * 4 + 3 * 8 - 7), False)),
+            (torch.ops.dava.l1_camera_vjp.default, args + (None, t(2, 3, 3 + 6 * 4 + 3 * 8 - 7), True)),
+        ]
     return out
+
+
+def test_functional_bfgs_solve_is_the_module_solve(device):
+    """torch.ops.dava.bfgs_solve (the functional entry SURVEY 8(b) names) is bitwise
+    BFGSSolver().eval() on the fused objective, and traces fullgraph under torch.compile."""
+    from deep_attention_visual_odometry_amd import BFGSSolver, ReprojectionError, make_scenes
+
+    s = make_scenes(8, 2, 64, seed=4343, drop=0.1)
+    obs = torch.tensor(s.observations, device=device)
+    vis = torch.tensor(s.visibility, device=device)
+    x0 = torch.tensor(s.initial, device=device)
+    solver = BFGSSolver(iterations=30).eval()
+    ref = solver(x0, ReprojectionError(obs, vis, 2, 64))
+    x, status = torch.ops.dava.bfgs_solve(x0, obs, vis.to(torch.uint8), 2, 64, iterations=30)
+    assert torch.equal(x, ref) and torch.equal(status, solver.last_status)
+    torch._dynamo.reset()
+    fn = torch.compile(lambda a: torch.ops.dava.bfgs_solve(a, obs, vis.to(torch.uint8), 2, 64, iterations=30)[0],
+                       fullgraph=True)
+    assert torch.equal(fn(x0), ref)
 
 
 def test_ops_pass_opcheck(device):

@@ -165,6 +165,8 @@ def test_fake_kernels_give_output_shapes_without_a_device():
         xo, err, st = torch.ops.dava.ba_solve(x, obs, vis, 2, 16, False, 1e-4, 0.9, -1.0, 7, -1.0, 1000, True, 1, 0,
                                               False, ws)
         assert xo.shape == x.shape and err.shape == (0,) and st.shape == (5, 4) and st.dtype == torch.int32
+        xo, st = torch.ops.dava.bfgs_solve(x, obs, vis, 2, 16)
+        assert xo.shape == x.shape and st.shape == (5, 4) and st.dtype == torch.int32
         e, g, sl = torch.ops.dava.ba_evaluate(x, obs, vis, 2, 16, False, x, None, True, True, 0)
         assert e.shape == (5,) and g.shape == x.shape and sl.shape == (5,)
         e, g, hv, og, ohv = torch.ops.dava.ba_second_order(x, obs, vis, 2, 16, False, None, 0, False, True)
@@ -186,6 +188,12 @@ def test_fake_kernels_give_output_shapes_without_a_device():
                                                    torch.empty(2, 4, 8, dtype=torch.uint8, device=dev),
                                                    0.1, 1e3, 1e3, 1.0, True, True)
         assert fe.shape == (2, 3) and fg.shape == (2, 3, 3 + 6 * 4 + 3 * 8 - 7)
+        vj = torch.ops.dava.l1_camera_vjp(*(torch.empty(2, 3, device=dev),) * 3, torch.empty(2, 3, 4, 3, device=dev),
+                                          torch.empty(2, 3, 4, 3, device=dev), torch.empty(2, 3, 6, 3, device=dev),
+                                          torch.empty(2, 4, 8, 2, device=dev),
+                                          torch.empty(2, 4, 8, dtype=torch.uint8, device=dev), 0.1, 1e3, 1e3, 1.0,
+                                          torch.empty(2, 3, device=dev), None, False)
+        assert vj.shape == (2, 3, 3 + 6 * 4 + 3 * 6)
         fn = ReprojectionError(obs, vis, 2, 16)
         out = BFGSSolver(iterations=7, error_threshold=-1.0, minimum_step=-1.0).eval()(x, fn)
         assert out.shape == x.shape and out.device.type == "cuda"
