@@ -616,6 +616,8 @@ __device__ __forceinline__ float wide_direction(int P, int Pv, int nh, const flo
 // entries in flight = more bytes outstanding per wave, which is what the history stream of a
 // problem with few waves (or few problems per CU) is bound by.
 #ifndef DAVA_FUSED_INFLIGHT_SMALL
+// (interleaved A/B, profiles/r02_ab_entries_in_flight.log: small 3 / 5 and large 3 are all slower
+// or within noise -- large 3 costs C3 8 %)
 #define DAVA_FUSED_INFLIGHT_SMALL 4  // rows of <= 2 float4 groups per lane (P <= 512)
 #endif
 #ifndef DAVA_FUSED_INFLIGHT_LARGE
