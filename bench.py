@@ -368,19 +368,25 @@ def main():
         dist.destroy_process_group()
 
 
-def adjoint_algorithmic_bytes(p: int, n: int) -> float:
+def adjoint_algorithmic_bytes(p: int, n: int, lds_entries: int = 0) -> float:
     """Minimum HBM bytes of the adjoint kernel for one problem of n steps (csrc/bfgs_adjoint.hip):
     reverse step k reads rows (a_j, g_j), j = k .. n-1, and history rows (s_j, w_j), j < k-1, once each,
-    plus x_k, g_k, g_{k-1}, s_{k-1}, w_{k-1} and the final a_k write: Pv floats per row."""
+    plus x_k, g_k, g_{k-1}, s_{k-1}, w_{k-1} and the final a_k write: Pv floats per row.  The oldest
+    `lds_entries` history entries are read once per problem into LDS and never again."""
     pv = (p + 3) // 4 * 4
-    rows = sum(2 * (n - k) + 2 * max(k - 1, 0) + 6 for k in range(1, n)) + 2
+    lh = min(lds_entries, max(n - 1, 0))
+    rows = sum(2 * (n - k) + 2 * max(k - 1 - lh, 0) + 6 for k in range(1, n)) + 2 + 2 * lh
     return 4.0 * pv * rows
 
 
 def differentiate_line(args, line, world, b, p, distortion, ray, phase_ms, st, finite, grads):
     fwd = float(np.mean([e[0].elapsed_time(e[1]) for e in phase_ms]))
     bwd = float(np.mean([e[1].elapsed_time(e[2]) for e in phase_ms]))
-    algo = b * adjoint_algorithmic_bytes(p, args.iterations)
+    from deep_attention_visual_odometry_amd import native_ops
+
+    lds_entries = native_ops.adjoint_lds_entries(b, args.views, args.points, distortion, args.iterations,
+                                                 1 if ray else 0)
+    algo = b * adjoint_algorithmic_bytes(p, args.iterations, lds_entries)
     achieved = algo / (bwd * 1e-3) / 1e9
     gx, gobs = grads
     line.update({
@@ -397,7 +403,9 @@ def differentiate_line(args, line, world, b, p, distortion, ray, phase_ms, st, f
         "roofline": {"kernel": "bfgs_ba_adjoint_kernel", "bound": "hbm", "achieved": round(achieved, 1),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
                      "byte_model": "adjoint: per reverse step k, rows (a_j, g_j) j >= k and history rows (s_j, w_j) "
-                                   "j < k-1 read once + 6 tape/workspace rows; its dual-number HVP is on top",
+                                   "j < k-1 read once + 6 tape/workspace rows; the oldest lds_entries history "
+                                   "entries are read once per problem; its dual-number HVP is on top",
+                     "lds_entries": lds_entries,
                      "algorithmic_bytes_per_launch": algo, "avg_launch_ms": round(bwd, 3)},
         "cpu_baseline": None,
         "parity": {"note": "gradient parity vs oracle autograd / the reference's goldens: tests/test_gpu_solve_grad.py"},

@@ -48,6 +48,7 @@ struct AdjointArgs {
   float* x0_grad;     // (B, P)
   float* obs_grad;    // (B, M, N, 2) or null
   float* arows;       // (B, K, Pv) workspace
+  int lcap;           // history entries (s_j, w_j), j < lcap, held in LDS for the H passes
 };
 
 constexpr int kAdjWaves = 4;
@@ -58,11 +59,13 @@ constexpr int kAdjInflight = DAVA_ADJ_INFLIGHT;  // entries per wave in flight i
 constexpr int kAdjBlock = kWave * kAdjWaves;
 
 struct AdjointCarve {
-  int xb, sbp, gbp, db, gk, p1, p2, wb, sv, wv, yv, gv, ak, an, sc, xd, gd, views, vpart, obs, obsacc, scratch,
+  int xb, sbp, gbp, db, gk, p1, p2, wb, sv, wv, yv, gv, ak, an, sc, xd, gd, views, vpart, obs, obsacc, lh, scratch,
       vis_bytes_off, total_bytes;
 };
 
-__host__ __device__ inline AdjointCarve carve_adjoint(int M, int N, int Pv, int T) {
+// lcap: the oldest history entries' rows (s_j, w_j interleaved) kept on chip for the whole reverse
+// sweep -- every H pass reads them again, so each one held saves 2 Pv floats of HBM per step
+__host__ __device__ inline AdjointCarve carve_adjoint(int M, int N, int Pv, int T, int lcap = 0) {
   AdjointCarve c;
   int off = 0;
   int* vec[] = {&c.xb, &c.sbp, &c.gbp, &c.db, &c.gk, &c.p1, &c.p2, &c.wb, &c.sv, &c.wv, &c.yv, &c.gv, &c.ak, &c.an};
@@ -74,6 +77,7 @@ __host__ __device__ inline AdjointCarve carve_adjoint(int M, int N, int Pv, int 
   c.vpart = off; off += 2 * round_up(vpart_floats(M, kAdjWaves), 4);
   c.obs = off; off += round_up(2 * M * N, 4);
   c.obsacc = off; off += round_up(2 * M * N, 4);
+  c.lh = off; off += 2 * lcap * Pv;
   c.scratch = off; off += 2 * kAdjWaves * 32;
   c.vis_bytes_off = off * 4;
   c.total_bytes = c.vis_bytes_off + round_up(M * N, 16);
@@ -94,11 +98,16 @@ __device__ __forceinline__ float dot4(f4a a, f4a b) {
 // in the fixed order (w0 + w2) + (w1 + w3), then base * (v1 | v2).  out / v / spares: LDS vectors.
 // Ends with a barrier.
 // R1_j0: if not null, entry j0's R1 row comes from this LDS vector instead of R1 + j0 Pv.
+// LR, nl: entries j < nl have both rows in LDS, R1 at LR + 2 j Pv, R2 at LR + (2 j + 1) Pv.
+// LDS-held rows are consumed in their own steps (each wave's entries in the same order), so the
+// HBM rows are read with global loads only: a generic pointer that may point at LDS makes flat
+// loads, which count on the LDS counter too and serialise every LDS read behind HBM latency.
 template <int GM, class Coef>
 __device__ __forceinline__ void pair_pass(int P, int Pv, int j0, int j1, const float* __restrict__ R1,
                                           const float* __restrict__ R2, const float* v1, const float* v2,
                                           float base, Coef coef, float* out1, float* out2, float* sp0, float* sp1,
-                                          float* sp2, float* sp3, const float* R1_j0 = nullptr) {
+                                          float* sp2, float* sp3, const float* R1_j0 = nullptr,
+                                          const float* LR = nullptr, int nl = 0) {
   const int lane = threadIdx.x & (kWave - 1);
   const int wave = threadIdx.x / kWave;
   const int G = (P + 3) / 4;
@@ -109,14 +118,16 @@ __device__ __forceinline__ void pair_pass(int P, int Pv, int j0, int j1, const f
     ok[m] = lane + kWave * m < G;
     pa[m] = pb[m] = f4a{0, 0, 0, 0};
   }
-  auto load = [&](int j, f4a (&r1)[GM], f4a (&r2)[GM]) {
+  auto load_from = [&](const float* r1p, const float* r2p, f4a (&r1)[GM], f4a (&r2)[GM]) {
 #pragma unroll
     for (int m = 0; m < GM; ++m) {
       const int q = lane + kWave * m;
-      const float* r1p = R1_j0 && j == j0 ? R1_j0 : R1 + (size_t)j * Pv;
       r1[m] = ok[m] ? ldv(r1p + 4 * q) : f4a{0, 0, 0, 0};
-      r2[m] = ok[m] ? ldv(R2 + (size_t)j * Pv + 4 * q) : f4a{0, 0, 0, 0};
+      r2[m] = ok[m] ? ldv(r2p + 4 * q) : f4a{0, 0, 0, 0};
     }
+  };
+  auto load = [&](int j, f4a (&r1)[GM], f4a (&r2)[GM]) {  // HBM rows
+    load_from(R1 + (size_t)j * Pv, R2 + (size_t)j * Pv, r1, r2);
   };
   auto consume = [&](int j, const f4a (&r1)[GM], const f4a (&r2)[GM]) {
     float d11 = 0.f, d21 = 0.f, d12 = 0.f, d22 = 0.f;
@@ -142,6 +153,17 @@ __device__ __forceinline__ void pair_pass(int P, int Pv, int j0, int j1, const f
   // EF entries of this wave in flight: at one wave per SIMD (the dual evaluation needs > 256
   // registers) the streams are latency-bound, and the register file has room for the rows
   int j = j0 + wave;
+  for (const int je = min(nl, j1); j < je; j += kAdjWaves) {  // LDS-held entries (wave-uniform)
+    f4a r1[GM], r2[GM];
+    load_from(LR + (size_t)2 * j * Pv, LR + (size_t)(2 * j + 1) * Pv, r1, r2);
+    consume(j, r1, r2);
+  }
+  if (R1_j0 && j == j0 && j < j1) {  // entry j0's R1 row in LDS (wave 0's first entry)
+    f4a r1[GM], r2[GM];
+    load_from(R1_j0, R2 + (size_t)j * Pv, r1, r2);
+    consume(j, r1, r2);
+    j += kAdjWaves;
+  }
   for (; j + (kAdjInflight - 1) * kAdjWaves < j1; j += kAdjInflight * kAdjWaves) {
     f4a r1[kAdjInflight][GM], r2[kAdjInflight][GM];
 #pragma unroll
@@ -204,7 +226,7 @@ __global__ __launch_bounds__(kAdjBlock, 1) void bfgs_ba_adjoint_kernel(AdjointAr
   const int P = L.P, M = L.M, N = L.N, MN = M * N, Pv = a.Pv, K = a.K;
   const int b = blockIdx.x, tid = threadIdx.x;
   const TapeLayout& tl = a.tl;
-  const AdjointCarve cv = carve_adjoint(M, N, Pv, tl.T);
+  const AdjointCarve cv = carve_adjoint(M, N, Pv, tl.T, a.lcap);
   float* xb = lds + cv.xb;    // xbar: adjoint of x_{k+1} entering step k, of x_k leaving it
   float* sbp = lds + cv.sbp;  // adjoint of s_k from the update that used it (step k + 1)
   float* gbp = lds + cv.gbp;  // adjoint of g_k from y_{k+1} = g_{k+1} - g_k
@@ -257,6 +279,13 @@ __global__ __launch_bounds__(kAdjBlock, 1) void bfgs_ba_adjoint_kernel(AdjointAr
   }
   for (int i = tid; i < MN; i += kAdjBlock) vis[i] = a.vis[(size_t)b * MN + i] ? 1 : 0;
   const int n = min(a.status[(size_t)b * DAVA_STATUS_WORDS], K);
+  float* lh = lds + cv.lh;
+  const int nlh = min(a.lcap, max(n - 1, 0));  // history entries 0 .. n-2 exist
+  for (int q = tid; q < nlh * (Pv / 4); q += kAdjBlock) {
+    const int j = q / (Pv / 4), i = 4 * (q % (Pv / 4));
+    stv(lh + (size_t)2 * j * Pv + i, ldv(S + (size_t)j * Pv + i));
+    stv(lh + (size_t)(2 * j + 1) * Pv + i, ldv(W + (size_t)j * Pv + i));
+  }
   const float gamma = sc[3 * K];
   float trace = 0.f;  // sum_{j > k} a_j . g_j with every a_j final (needed at k = 1: gamma's adjoint)
   int buf = 0;
@@ -320,7 +349,7 @@ __global__ __launch_bounds__(kAdjBlock, 1) void bfgs_ba_adjoint_kernel(AdjointAr
                         k1 = cr * sdv - rj * wdv; k2 = -rj * sdv;
                         k3 = cr * swv - rj * wwv; k4 = -rj * swv;
                       },
-                      hd, hw, sp0, sp1, sp2, sp3);
+                      hd, hw, sp0, sp1, sp2, sp3, nullptr, lh, nlh);
       } else {
         for (int i = tid; i < Pv; i += kAdjBlock) {
           hd[i] = gamma * db[i];
@@ -393,6 +422,8 @@ static void launch_adjoint(const AdjointArgs& a, int B, int lds, int gm, hipStre
   else go(bfgs_ba_adjoint_kernel<RES, 4>);
 }
 
+constexpr int kAdjLdsBytes = 160 * 1024;
+
 static int adjoint_check(const DavaScene* s, const DavaSolverConfig* c) {
   if (!s || !c) return DAVA_ERR_INVALID_ARGUMENT;
   if (s->batch < 0 || s->num_views < 2 || s->num_points < 1) return DAVA_ERR_INVALID_ARGUMENT;
@@ -403,8 +434,18 @@ static int adjoint_check(const DavaScene* s, const DavaSolverConfig* c) {
   if (s->residual == DAVA_RESIDUAL_RAY_ANGLE && s->distortion) return DAVA_ERR_UNSUPPORTED;
   if (c->hessian_mode != DAVA_HESSIAN_COMPACT || c->iterations < 1 || P > 1024) return DAVA_ERR_UNSUPPORTED;
   const TapeLayout tl = tape_layout(s->batch, P, c->iterations);
-  if (carve_adjoint(s->num_views, s->num_points, tl.Pv, tl.T).total_bytes > 160 * 1024) return DAVA_ERR_UNSUPPORTED;
+  if (carve_adjoint(s->num_views, s->num_points, tl.Pv, tl.T).total_bytes > kAdjLdsBytes) return DAVA_ERR_UNSUPPORTED;
   return DAVA_OK;
+}
+
+// As many history entries on chip as the CU's LDS leaves room for (one workgroup per CU), at most
+// the K - 1 a solve can make; DAVA_ADJ_LDS_ENTRIES caps it (0: none) for A/B runs.
+static int adjoint_lds_entries(const DavaScene* s, const TapeLayout& tl) {
+  const int base = carve_adjoint(s->num_views, s->num_points, tl.Pv, tl.T).total_bytes;
+  int n = (kAdjLdsBytes - base) / (int)(2 * tl.Pv * sizeof(float));
+  n = max(0, min(n, tl.K - 1));
+  if (const char* e = getenv("DAVA_ADJ_LDS_ENTRIES")) n = max(0, min(n, atoi(e)));
+  return n;
 }
 
 }  // namespace dava
@@ -415,6 +456,11 @@ extern "C" size_t dava_ba_solve_backward_workspace_bytes(const DavaScene* scene,
   if (adjoint_check(scene, config) != DAVA_OK) return 0;
   const TapeLayout tl = tape_layout(scene->batch, scene->num_parameters, config->iterations);
   return (size_t)scene->batch * tl.K * tl.Pv * sizeof(float) + 256;
+}
+
+extern "C" int dava_ba_solve_backward_lds_entries(const DavaScene* scene, const DavaSolverConfig* config) {
+  if (adjoint_check(scene, config) != DAVA_OK) return 0;
+  return adjoint_lds_entries(scene, tape_layout(scene->batch, scene->num_parameters, config->iterations));
 }
 
 extern "C" int dava_ba_solve_backward(const DavaScene* scene, const DavaSolverConfig* config, const void* tape,
@@ -442,7 +488,8 @@ extern "C" int dava_ba_solve_backward(const DavaScene* scene, const DavaSolverCo
   a.x0_grad = x0_grad;
   a.obs_grad = observations_grad;
   a.arows = static_cast<float*>(workspace);
-  const int lds = carve_adjoint(scene->num_views, scene->num_points, tl.Pv, tl.T).total_bytes;
+  a.lcap = adjoint_lds_entries(scene, tl);
+  const int lds = carve_adjoint(scene->num_views, scene->num_points, tl.Pv, tl.T, a.lcap).total_bytes;
   const int gm = (tl.Pv / 4 + kWave - 1) / kWave;
   hipStream_t s = static_cast<hipStream_t>(stream);
   if (scene->residual == DAVA_RESIDUAL_RAY_ANGLE) launch_adjoint<DAVA_RESIDUAL_RAY_ANGLE>(a, scene->batch, lds, gm, s);

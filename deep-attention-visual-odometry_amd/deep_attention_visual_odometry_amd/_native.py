@@ -83,6 +83,7 @@ SIGNATURES = {
                                                                  ctypes.POINTER(DavaSolverConfig)]),
     "dava_ba_solve_backward": (ctypes.c_int, [ctypes.POINTER(DavaScene), ctypes.POINTER(DavaSolverConfig), _vp,
                                               ctypes.c_size_t, _vp, _vp, _vp, _vp, _vp, ctypes.c_size_t, _vp]),
+    "dava_ba_solve_backward_lds_entries": (ctypes.c_int, [ctypes.POINTER(DavaScene), ctypes.POINTER(DavaSolverConfig)]),
     "dava_abi_version": (ctypes.c_int, []),
     "dava_status_string": (ctypes.c_char_p, [ctypes.c_int]),
     "dava_device_arch": (ctypes.c_char_p, []),

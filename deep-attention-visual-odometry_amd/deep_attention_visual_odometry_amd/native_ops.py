@@ -165,6 +165,15 @@ def solve_plan(batch: int, num_views: int, num_points: int, distortion: bool,
     return {name: int(getattr(plan, name)) for name, _ in N.DavaSolvePlan._fields_}
 
 
+def adjoint_lds_entries(batch: int, num_views: int, num_points: int, distortion: bool, iterations: int,
+                        residual: int = N.DAVA_RESIDUAL_SQUARED_REPROJECTION) -> int:
+    """History entries the fused solve's adjoint keeps on chip (``dava_ba_solve_backward_lds_entries``);
+    0 where the adjoint does not run."""
+    sc = scene_struct(None, None, num_views, num_points, distortion, batch, residual)
+    cfg = solver_config(1e-4, 0.9, -1.0, iterations, -1.0, 1000, True, N.DAVA_HESSIAN_COMPACT)
+    return int(N.load_library().dava_ba_solve_backward_lds_entries(sc, cfg))
+
+
 # ---- generic BFGS building blocks ----
 # Each public op is a torch.autograd.Function whose forward AND backward are torch.ops.dava
 # operators (HIP kernels, bfgs_ops.hip / bfgs_grad.hip), so the drop-in solver can be

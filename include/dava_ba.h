@@ -157,6 +157,11 @@ int dava_ba_solve_record(const DavaScene* scene, const DavaSolverConfig* config,
 /* Device workspace of dava_ba_solve_backward, or 0 if unsupported. */
 size_t dava_ba_solve_backward_workspace_bytes(const DavaScene* scene, const DavaSolverConfig* config);
 
+/* History entries (s_j, w_j) the adjoint keeps in LDS for its whole reverse sweep (the oldest
+ * ones, as many as one workgroup's LDS leaves room for, at most iterations - 1; the
+ * DAVA_ADJ_LDS_ENTRIES environment variable caps it).  Informational: for byte models. */
+int dava_ba_solve_backward_lds_entries(const DavaScene* scene, const DavaSolverConfig* config);
+
 /* Vector-Jacobian product of the recorded solve: given x_out_grad = dL/dx_out (B, P), writes
  *   x0_grad            (B, P)        dL/dx0
  *   observations_grad  (B, M, N, 2)  dL/dobs (or NULL)
