@@ -1116,6 +1116,11 @@ __global__ __launch_bounds__(kWave * NW, DAVA_SOLVE_WAVES_PER_EU) void bfgs_ba_s
           if (k - 1 < lcap) {
             float* sr = LH + (size_t)2 * (k - 1) * Pv;
             for (int i = tid; i < Pv; i += BLOCK) { sr[i] = s_cur[i]; sr[Pv + i] = hy_new[i]; }
+            if (a.tape_x) {  // recording: the tape keeps every entry (the reads stay on chip)
+              float* tsr = SH + (size_t)(k - 1) * Pv;
+              float* twr = WH + (size_t)(k - 1) * Pv;
+              for (int i = tid; i < Pv; i += BLOCK) { tsr[i] = s_cur[i]; twr[i] = hy_new[i]; }
+            }
           } else {
             float* sr = SH + (size_t)(k - 1) * Pv;
             float* wr = WH + (size_t)(k - 1) * Pv;
@@ -1547,7 +1552,7 @@ static int solve_impl(const DavaScene* scene, const DavaSolverConfig* config, co
   const bool xl = use_xl(scene, kcap, gv);
   const int nw = solve_waves_for(scene, gv, mode);
   // recording keeps every history entry in HBM (the adjoint reads them back; bitwise the same run)
-  const int lcap = mode == DAVA_HESSIAN_COMPACT && !record ? lds_history_entries(scene, kcap, gv, nw) : 0;
+  const int lcap = mode == DAVA_HESSIAN_COMPACT ? lds_history_entries(scene, kcap, gv, nw) : 0;
   const int lds = lds_bytes_for(scene, kcap, gv, lcap, xl, nw);
   if (lds > kMaxLds) return DAVA_ERR_UNSUPPORTED;
   const size_t vec = gv ? gv_vector_bytes(scene) : 0;
