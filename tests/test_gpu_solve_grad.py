@@ -372,6 +372,31 @@ def test_recording_tape_is_deterministic(device):
     assert torch.equal(tape, first)
 
 
+def test_adjoint_on_chip_history_is_bitwise_invisible(device, monkeypatch):
+    """The adjoint's LDS-held history entries (dava_ba_solve_backward_lds_entries) change where rows
+    are read from, not the arithmetic: 0, 3 and the default count give identical gradients."""
+    from deep_attention_visual_odometry_amd import make_scenes, native_ops
+
+    m, n, k = 4, 256, 24
+    assert native_ops.adjoint_lds_entries(8, m, n, True, k) > 3
+    s = make_scenes(8, m, n, distortion=True, seed=935, drop=0.0)  # (with drop 0.1, 3 of these 8 walk to
+    # NaN in the first line search -- in the oracle too -- and NaN != NaN)
+    x0, obs, vis = (torch.tensor(t).to(device) for t in (s.initial, s.observations, s.visibility))
+    vis = vis.to(torch.uint8)
+    w = torch.randn(x0.shape, generator=torch.Generator().manual_seed(5)).to(device)
+    x, status, tape = torch.ops.dava.ba_solve_record(x0, obs, vis, m, n, True, 1e-4, 0.9, -1.0, k, -1.0, 1000, True, 0)
+    assert (status[:, 0] == k).all() and torch.isfinite(x).all()
+    runs = []
+    for cap in (None, "0", "3"):
+        if cap is None:
+            monkeypatch.delenv("DAVA_ADJ_LDS_ENTRIES", raising=False)
+        else:
+            monkeypatch.setenv("DAVA_ADJ_LDS_ENTRIES", cap)
+        runs.append(torch.ops.dava.ba_solve_backward(w, tape, status, obs, vis, m, n, True, k, 0, True))
+    for gx, gobs in runs[1:]:
+        assert torch.equal(gx, runs[0][0]) and torch.equal(gobs, runs[0][1])
+
+
 def test_fused_and_generic_backward_agree_c3(device, monkeypatch):
     """C3 + Brown-Conrady, K = 30: the adjoint kernel and the generic loop (dense H per iteration in
     torch's graph, HIP VJP kernels) give the same gradients."""
