@@ -15,7 +15,9 @@ Autograd through the model's error/gradient tensors follows the reference's
 HIP VJP kernel (``dava_l1_camera_vjp``: one forward-mode dual-number pass per input element,
 contracted with the cotangents in-kernel).  With ``enable_error_gradients=False`` the error is
 returned detached; with ``enable_grad_gradients=False`` the gradient is differentiated with the
-world and camera-relative points held constant, as the reference's detaches do.  Gradients
+world and camera-relative points held constant, as the reference's detaches do -- on a full
+evaluation only: its partial recompute of masked estimates (``:223-270``) detaches nothing, and
+neither does this one.  Gradients
 into ``true_projected_points`` are not provided: if it requires grad under grad mode,
 evaluation raises.
 """
@@ -152,7 +154,7 @@ class PinholeCameraModelL1(IOptimisableFunction):
         return self._cy
 
     # ---- evaluation (HIP) ----
-    def _evaluate(self, want_error: bool, want_gradient: bool):
+    def _evaluate(self, want_error: bool, want_gradient: bool, detach_points: Optional[bool] = None):
         N.require_device_tensor(self._focal_length, "focal_length")
         inputs = (self._focal_length, self._cx, self._cy, self._translation, self._orientation.lie_vector,
                   self._world_points)
@@ -180,7 +182,8 @@ class PinholeCameraModelL1(IOptimisableFunction):
         target = cast(self._true_projected_points.detach()).reshape(b, m, n, 2)
         vis = _c(self._visibility_mask.detach().to(device=dev, dtype=torch.uint8)).reshape(b, m, n)
         fixed = (target, vis, float(self.minimum_z_distance), float(self.maximum_pixel_ratio),
-                 float(self._max_gradient), float(self._error_scale.item()), not self._enable_grad_gradients)
+                 float(self._max_gradient), float(self._error_scale.item()),
+                 (not self._enable_grad_gradients) if detach_points is None else bool(detach_points))
         if differentiable:
             err, grad = _L1Evaluate.apply(fixed, bool(want_error), bool(want_gradient), focal, cx, cy, trans, lie,
                                           world)
@@ -207,7 +210,8 @@ class PinholeCameraModelL1(IOptimisableFunction):
     def get_gradient(self) -> torch.Tensor:
         """The reference's hand-written gradient per estimate, (B, E, P) (``:192-285``)."""
         if self._gradient is None or self._gradient_mask is not None:
-            _, grad = self._evaluate(False, True)
+            # the reference's partial recompute (:223-270) applies no enable_grad_gradients detach
+            _, grad = self._evaluate(False, True, detach_points=False if self._gradient is not None else None)
             if self._gradient is not None:
                 grad = torch.where(self._gradient_mask.unsqueeze(-1), self._gradient, grad)
             self._gradient = grad

@@ -520,6 +520,40 @@ def gen_camera_l1_autograd():
             out[tag + "_error_requires_grad"] = np.array(err.requires_grad)
             for k, g in zip(names, got):
                 out[f"{tag}_d_{k}"] = (g if g is not None else torch.zeros_like(leaves[k])).numpy()
+    # gradients THROUGH the legacy solver (BFGSCameraSolver + LineSearchStrongWolfeConditions over
+    # the model), the GuessAndSolverModel training path: d(sum w . solved parameters)/d(initial ones)
+    from deep_attention_visual_odometry.solvers import BFGSCameraSolver
+    from deep_attention_visual_odometry.solvers.line_search_strong_wolfe_conditions import (
+        LineSearchStrongWolfeConditions,
+    )
+
+    m, n = 4, 8
+    _, parts, true, vis = _l1_model(np.random.default_rng(9401), 3, 1, m, n, torch.float64, max_gradient=1e3)
+    for k, v in parts.items():
+        out[f"solve_{k}"] = v.numpy()
+    out["solve_true"], out["solve_vis"] = true.numpy(), vis.numpy()
+    for flags in ((True, True), (True, False)):
+        leaves = {k: parts[k].clone().requires_grad_(True) for k in names}
+        model = PinholeCameraModelL1(
+            focal_length=leaves["focal_length"], cx=leaves["cx"], cy=leaves["cy"],
+            translation=leaves["translation"], orientation=LieRotation(leaves["lie"]),
+            world_points=leaves["world"], true_projected_points=true, visibility_mask=vis, max_gradient=1e3,
+            constrain=True, enable_error_gradients=flags[0], enable_grad_gradients=flags[1])
+        solver = BFGSCameraSolver(max_iterations=3, epsilon=1e-6, max_step_distance=1e3, min_step_distance=1e-3,
+                                  line_search=LineSearchStrongWolfeConditions(max_step_size=1e5, zoom_iterations=20,
+                                                                              sufficient_decrease=1e-4,
+                                                                              curvature=0.9),
+                                  search_direction_network=None)
+        res = solver(model)
+        outs = [res.focal_length, res.cx, res.cy, res._translation, res._orientation._lie_vector, res._world_points]
+        gen = torch.Generator().manual_seed(6)
+        loss = sum((o * torch.randn(o.shape, generator=gen, dtype=o.dtype)).sum() for o in outs)
+        got = torch.autograd.grad(loss, [leaves[k] for k in names], allow_unused=True)
+        tag = f"solve_{int(flags[0])}{int(flags[1])}"
+        for k, o in zip(names, outs):
+            out[f"{tag}_out_{k}"] = o.detach().numpy()
+        for k, g in zip(names, got):
+            out[f"{tag}_d_{k}"] = (g if g is not None else torch.zeros_like(leaves[k])).numpy()
     np.savez_compressed(os.path.join(HERE, "camera_l1_autograd.npz"), **out)
 
 

@@ -279,6 +279,40 @@ def test_autograd_through_the_model_matches_reference(device, case, flags):
         assert (a.cpu() - want).abs().max().item() <= 1e-9 * scale, (case, flags, k)
 
 
+@pytest.mark.parametrize("flags", ["11", "10"])
+def test_gradients_through_the_legacy_solver_match_reference(device, flags):
+    """Training through the legacy path (GuessAndSolverModel: BFGSCameraSolver +
+    LineSearchStrongWolfeConditions over PinholeCameraModelL1, 3 iterations, fp64): the solved
+    parameters and d(sum w . solved)/d(initial parameters) against the reference's own autograd
+    (tests/golden/camera_l1_autograd.npz, solve_*)."""
+    from deep_attention_visual_odometry_amd.camera_model import PinholeCameraModelL1
+    from deep_attention_visual_odometry_amd.geometry import LieRotation
+    from deep_attention_visual_odometry_amd.solvers import BFGSCameraSolver, LineSearchStrongWolfeConditions
+
+    g = np.load(os.path.join(GOLDEN, "camera_l1_autograd.npz"))
+    leaves = {k: torch.tensor(g[f"solve_{k}"], device=device).requires_grad_(True) for k in PARAMS}
+    model = PinholeCameraModelL1(
+        focal_length=leaves["focal_length"], cx=leaves["cx"], cy=leaves["cy"], translation=leaves["translation"],
+        orientation=LieRotation(leaves["lie"]), world_points=leaves["world"],
+        true_projected_points=torch.tensor(g["solve_true"], device=device),
+        visibility_mask=torch.tensor(g["solve_vis"], device=device), max_gradient=1e3, constrain=True,
+        enable_error_gradients=flags[0] == "1", enable_grad_gradients=flags[1] == "1")
+    solver = BFGSCameraSolver(max_iterations=3, epsilon=1e-6, max_step_distance=1e3, min_step_distance=1e-3,
+                              line_search=LineSearchStrongWolfeConditions(max_step_size=1e5, zoom_iterations=20,
+                                                                          sufficient_decrease=1e-4, curvature=0.9))
+    res = solver(model)
+    outs = [res.focal_length, res.cx, res.cy, res._translation, res._orientation.lie_vector, res._world_points]
+    gen = torch.Generator().manual_seed(6)
+    loss = sum((o * torch.randn(o.shape, generator=gen, dtype=o.dtype).to(device)).sum() for o in outs)
+    got = torch.autograd.grad(loss, [leaves[k] for k in PARAMS], allow_unused=True)
+    for k, o in zip(PARAMS, outs):
+        assert _rel(o.detach(), torch.tensor(g[f"solve_{flags}_out_{k}"])) < 1e-9, k
+    for k, d in zip(PARAMS, got):
+        want = torch.tensor(g[f"solve_{flags}_d_{k}"])
+        d = d if d is not None else torch.zeros_like(want)
+        assert (d.cpu() - want).abs().max().item() <= 1e-7 * max(want.abs().max().item(), 1.0), (flags, k)
+
+
 def test_autograd_through_the_model_float32(device):
     """float32 model, against the float64 oracle (fp32-rounded inputs)."""
     m, n, kw = AUTOGRAD_CASES["mg20"]
