@@ -53,6 +53,10 @@ __device__ unsigned long long g_eval_cycles[kEvalSections];
   } while (0)
 #endif
 
+// Two points' worth of fp32 in one register pair: the packed pair sweep (PACK) runs the
+// per-(view, point) arithmetic on v_pk_{fma,mul,add}_f32, two points per instruction.
+typedef float pf2 __attribute__((ext_vector_type(2)));
+
 struct Layout {
   int M, N, P, distort;
   __device__ __forceinline__ int pt(int n) const { return 3 + 3 * n; }
@@ -219,7 +223,8 @@ __device__ __forceinline__ void ray_angle_pair(const RayAngle<S>& ra, const floa
 //        gradients in registers for the whole view sweep (requires N <= PPT * threads);
 //        PPT = 0: they are re-read from / accumulated into x, d, grad view after view.
 template <bool GRAD, bool SLOPE, bool TRIAL, bool DOT = false, bool CHECK = false,
-          int RES = DAVA_RESIDUAL_SQUARED_REPROJECTION, typename S = float, int NW = kWaves, int PPT = 0>
+          int RES = DAVA_RESIDUAL_SQUARED_REPROJECTION, typename S = float, int NW = kWaves, int PPT = 0,
+          bool PACK = false>
 __device__ __forceinline__ bool ba_eval(const Layout& L, const S* x, const S* d, float alpha, const float* obs,
                                         const uint8_t* vis, S* grad, S* views, S* vpart, float* scratch, int& buf,
                                         S& E_out, S& slope_out, S* obs_grad = nullptr,
@@ -528,6 +533,10 @@ __device__ __forceinline__ bool ba_eval(const Layout& L, const S* x, const S* d,
         }
       }
     };
+    // PACK: two of this thread's points (n0, n1 = n0 + BLOCK) per step, the same formulas as
+    // `pair` (squared reprojection, fp32) on packed pairs.  Every accumulator still takes point n0's
+    // term, then n1's -- the order of the scalar sweep; only the rounding of FMA contraction
+    // inside a term may differ from the scalar form.
     if constexpr (PPT > 0) {
 #pragma unroll
       for (int u = 0; u < PPT; ++u) {
@@ -535,7 +544,154 @@ __device__ __forceinline__ bool ba_eval(const Layout& L, const S* x, const S* d,
         if (n < N) pair(n, Xr[u][0], Xr[u][1], Xr[u][2], Dr[u][0], Dr[u][1], Dr[u][2], Gr[u][0], Gr[u][1], Gr[u][2]);
       }
     } else {
-      for (int n = tid; n < N; n += BLOCK) {
+      int n0 = tid;
+      if constexpr (PACK && RES == DAVA_RESIDUAL_SQUARED_REPROJECTION && std::is_same<S, float>::value) {
+        auto pair2 = [&](int n0, int n1, const pf2 X0, const pf2 X1, const pf2 X2, const pf2 dX0, const pf2 dX1,
+                         const pf2 dX2, pf2& q0, pf2& q1, pf2& q2) {
+          const int i0 = m * N + n0, i1 = m * N + n1;
+          const pf2 obu = {obs[2 * i0], obs[2 * i1]}, obv = {obs[2 * i0 + 1], obs[2 * i1 + 1]};
+          const pf2 wgt = {vis[i0] ? 1.0f : 0.0f, vis[i1] ? 1.0f : 0.0f};
+          auto acc = [](S& a, const pf2 t) {
+            a += t.x;
+            a += t.y;
+          };
+          const pf2 a0 = X0 * inv_s, a1 = X1 * inv_s, a2 = X2 * inv_s;
+          pf2 da0 = 0.f, da1 = 0.f, da2 = 0.f;
+          if constexpr (SLOPE) {
+            da0 = (dX0 - a0 * (ds_over_s * s)) * inv_s;
+            da1 = (dX1 - a1 * (ds_over_s * s)) * inv_s;
+            da2 = (dX2 - a2 * (ds_over_s * s)) * inv_s;
+          }
+          pf2 p0, p1, p2, dp0 = 0.f, dp1 = 0.f, dp2 = 0.f;
+          pf2 vw = 0.f, c0 = 0.f, c1 = 0.f, c2 = 0.f;
+          if (m == 0) {
+            p0 = a0; p1 = a1; p2 = a2;
+            if constexpr (SLOPE) { dp0 = da0; dp1 = da1; dp2 = da2; }
+          } else {
+            vw = a0 * w0 + a1 * w1 + a2 * w2;
+            c0 = w1 * a2 - w2 * a1;
+            c1 = w2 * a0 - w0 * a2;
+            c2 = w0 * a1 - w1 * a0;
+            const pf2 Avw = vA * vw;
+            p0 = a0 * vc + Avw * w0 + c0 * vB + tt0;
+            p1 = a1 * vc + Avw * w1 + c1 * vB + tt1;
+            p2 = a2 * vc + Avw * w2 + c2 * vB + tt2;
+            if constexpr (SLOPE) {
+              const S dc = -vs * dth, dA = vAp * dth, dB = vTC * dth;
+              const pf2 dvw = (da0 * w0 + da1 * w1 + da2 * w2) + (a0 * dw0 + a1 * dw1 + a2 * dw2);
+              const pf2 e0 = (dw1 * a2 - dw2 * a1) + (w1 * da2 - w2 * da1);
+              const pf2 e1 = (dw2 * a0 - dw0 * a2) + (w2 * da0 - w0 * da2);
+              const pf2 e2 = (dw0 * a1 - dw1 * a0) + (w0 * da1 - w1 * da0);
+              const pf2 k = dA * vw + vA * dvw;
+              dp0 = da0 * vc + a0 * dc + k * w0 + Avw * dw0 + e0 * vB + c0 * dB + dtt0;
+              dp1 = da1 * vc + a1 * dc + k * w1 + Avw * dw1 + e1 * vB + c1 * dB + dtt1;
+              dp2 = da2 * vc + a2 * dc + k * w2 + Avw * dw2 + e2 * vB + c2 * dB + dtt2;
+            }
+          }
+          const pf2 iz = 1.0f / p2;
+          const pf2 qx = p0 * iz, qy = p1 * iz;
+          const pf2 ub = in.f * qx, vb = in.f * qy;
+          pf2 u, vv, dub = 0.f, dvb = 0.f;
+          pf2 Juu = 1.f, Juv = 0.f, Jvv = 1.f, r2 = 0.f;
+          if constexpr (SLOPE) {
+            const pf2 dqx = (dp0 - qx * dp2) * iz, dqy = (dp1 - qy * dp2) * iz;
+            dub = din.f * qx + in.f * dqx;
+            dvb = din.f * qy + in.f * dqy;
+          }
+          if (L.distort) {
+            r2 = ub * ub + vb * vb;
+            const pf2 D = 1.0f + in.k1 * r2 + in.k2 * r2 * r2 + in.k3 * r2 * r2 * r2;
+            const pf2 Dr = in.k1 + 2.0f * in.k2 * r2 + 3.0f * in.k3 * r2 * r2;
+            const pf2 uvb = ub * vb;
+            u = ub * D + 2.0f * in.p1 * uvb + in.p2 * (r2 + 2.0f * ub * ub) + in.cx;
+            vv = vb * D + 2.0f * in.p2 * uvb + in.p1 * (r2 + 2.0f * vb * vb) + in.cy;
+            Juu = D + 2.0f * ub * ub * Dr + 2.0f * in.p1 * vb + 6.0f * in.p2 * ub;
+            Juv = 2.0f * uvb * Dr + 2.0f * in.p1 * ub + 2.0f * in.p2 * vb;
+            Jvv = D + 2.0f * vb * vb * Dr + 2.0f * in.p2 * ub + 6.0f * in.p1 * vb;
+          } else {
+            u = ub + in.cx;
+            vv = vb + in.cy;
+          }
+          const pf2 ru = u - obu, rv = vv - obv;
+          acc(e_loc, (ru * ru + rv * rv) * wgt);
+          if constexpr (SLOPE) {
+            pf2 du = Juu * dub + Juv * dvb + din.cx;
+            pf2 dv = Juv * dub + Jvv * dvb + din.cy;
+            if (L.distort) {
+              const pf2 r4 = r2 * r2;
+              du += ub * (r2 * din.k1 + r4 * din.k2 + r4 * r2 * din.k3) + 2.0f * ub * vb * din.p1 +
+                    (r2 + 2.0f * ub * ub) * din.p2;
+              dv += vb * (r2 * din.k1 + r4 * din.k2 + r4 * r2 * din.k3) + (r2 + 2.0f * vb * vb) * din.p1 +
+                    2.0f * ub * vb * din.p2;
+            }
+            acc(sl_loc, 2.0f * wgt * (ru * du + rv * dv));
+          }
+          if constexpr (GRAD) {
+            const pf2 gu = 2.0f * wgt * ru, gv = 2.0f * wgt * rv;
+            acc(gin[1], gu);
+            acc(gin[2], gv);
+            pf2 gub = gu, gvb = gv;
+            if (L.distort) {
+              gub = gu * Juu + gv * Juv;
+              gvb = gu * Juv + gv * Jvv;
+              const pf2 r4 = r2 * r2;
+              const pf2 gr = gu * ub + gv * vb;
+              acc(gin[3], gr * r2);
+              acc(gin[4], gr * r4);
+              acc(gin[5], gr * r4 * r2);
+              acc(gin[6], gu * 2.0f * ub * vb + gv * (r2 + 2.0f * vb * vb));
+              acc(gin[7], gu * (r2 + 2.0f * ub * ub) + gv * 2.0f * ub * vb);
+            }
+            acc(gin[0], gub * qx + gvb * qy);
+            const pf2 fi = in.f * iz;
+            const pf2 G0 = gub * fi, G1 = gvb * fi, G2 = -(gub * ub + gvb * vb) * iz;
+            pf2 gx0, gx1, gx2;
+            if (m == 0) {
+              gx0 = G0; gx1 = G1; gx2 = G2;
+            } else {
+              const pf2 Gw = G0 * w0 + G1 * w1 + G2 * w2;
+              const pf2 Gv = G0 * a0 + G1 * a1 + G2 * a2;
+              const pf2 Gx = G0 * c0 + G1 * c1 + G2 * c2;
+              const pf2 AGw = vA * Gw, Avw = vA * vw;
+              gx0 = vc * G0 + AGw * w0 + vB * (G1 * w2 - G2 * w1);
+              gx1 = vc * G1 + AGw * w1 + vB * (G2 * w0 - G0 * w2);
+              gx2 = vc * G2 + AGw * w2 + vB * (G0 * w1 - G1 * w0);
+              acc(vg[0], Avw * G0 + AGw * a0 + vB * (a1 * G2 - a2 * G1));
+              acc(vg[1], Avw * G1 + AGw * a1 + vB * (a2 * G0 - a0 * G2));
+              acc(vg[2], Avw * G2 + AGw * a2 + vB * (a0 * G1 - a1 * G0));
+              acc(vg[3], -vs * Gv + vAp * vw * Gw + vTC * Gx);
+              acc(vg[4], G0); acc(vg[5], G1); acc(vg[6], G2);
+            }
+            if (m == 0) { q0 = gx0; q1 = gx1; q2 = gx2; }
+            else { q0 += gx0; q1 += gx1; q2 += gx2; }
+            if (m == M - 1) {
+              acc(gsx, q0 * X0 + q1 * X1 + q2 * X2);
+              if constexpr (DOT) acc(gdx, q0 * dX0 + q1 * dX1 + q2 * dX2);
+            }
+          }
+        };
+        for (; n0 + BLOCK < N; n0 += 2 * BLOCK) {
+          const int n1 = n0 + BLOCK, ia = L.pt(n0), ib = L.pt(n1);
+          pf2 X[3], dX[3] = {0.f, 0.f, 0.f}, q[3] = {0.f, 0.f, 0.f};
+#pragma unroll
+          for (int c = 0; c < 3; ++c) {
+            X[c] = pf2{trial_value<TRIAL>(x, d, alpha, ia + c), trial_value<TRIAL>(x, d, alpha, ib + c)};
+            if constexpr (SLOPE || DOT) dX[c] = pf2{d[ia + c], d[ib + c]};
+            if constexpr (GRAD) {
+              if (m > 0) q[c] = pf2{grad[ia + c], grad[ib + c]};
+            }
+          }
+          pair2(n0, n1, X[0], X[1], X[2], dX[0], dX[1], dX[2], q[0], q[1], q[2]);
+          if constexpr (GRAD) {
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+              grad[ia + c] = q[c].x;
+              grad[ib + c] = q[c].y;
+            }
+          }
+        }
+      }
+      for (int n = n0; n < N; n += BLOCK) {
         const int ip = L.pt(n);
         const S X0 = trial_value<TRIAL>(x, d, alpha, ip + 0);
         const S X1 = trial_value<TRIAL>(x, d, alpha, ip + 1);

@@ -165,6 +165,11 @@ __device__ __forceinline__ void st4(float* p, float4 v) { *reinterpret_cast<floa
 #ifndef DAVA_DIAG_NO_SWEEP
 #define DAVA_DIAG_NO_SWEEP 0
 #endif
+// GV mode (C5: N = 4096 points, eight per thread): the objective's pair sweep takes two points per
+// step on packed fp32 arithmetic (ba_eval PACK).  0: the scalar sweep.
+#ifndef DAVA_PACKED_PAIRS
+#define DAVA_PACKED_PAIRS 1
+#endif
 #ifndef DAVA_TRIAL_DOT
 #define DAVA_TRIAL_DOT 0  // 1: trial slope as d . grad (reverse mode); 0: forward-mode JVP
 #endif
@@ -974,7 +979,7 @@ __global__ __launch_bounds__(kWave * NW, DAVA_SOLVE_WAVES_PER_EU) void bfgs_ba_s
       if (have_next) {
         E = E_next;
       } else {
-        ba_eval<true, false, false, false, false, RES, float, NW, PPT>(L, x, nullptr, 0.f, obs, vis, grad_buf(g), views, vpart,
+        ba_eval<true, false, false, false, false, RES, float, NW, PPT, GV && DAVA_PACKED_PAIRS>(L, x, nullptr, 0.f, obs, vis, grad_buf(g), views, vpart,
                                                                   scratch, buf, E, unused);
         publish(g);
         ++evals;
@@ -1171,7 +1176,8 @@ __global__ __launch_bounds__(kWave * NW, DAVA_SOLVE_WAVES_PER_EU) void bfgs_ba_s
         // next iterate's gradient) and phi'(alpha) = d . grad (DOT).
         const bool known_same = DAVA_TRIAL_CHECK && al <= nomove_al;  // uniform
         if (!known_same &&
-            ba_eval<true, !DAVA_TRIAL_DOT, true, DAVA_TRIAL_DOT, DAVA_TRIAL_CHECK, RES, float, NW, PPT>(
+            ba_eval<true, !DAVA_TRIAL_DOT, true, DAVA_TRIAL_DOT, DAVA_TRIAL_CHECK, RES, float, NW, PPT,
+                    GV && DAVA_PACKED_PAIRS>(
                 L, x, d, al, obs, vis, grad_buf(gp), views, vpart, scratch, buf, fa, dfa)) {
           ++evals;
           last_same = false;
@@ -1250,7 +1256,7 @@ __global__ __launch_bounds__(kWave * NW, DAVA_SOLVE_WAVES_PER_EU) void bfgs_ba_s
     for (int i = tid; i < P; i += BLOCK) xo[i] = x[i];
     if (a.err_out) {
       float e2 = 0.f;
-      ba_eval<false, false, false, false, false, RES, float, NW, PPT>(L, x, nullptr, 0.f, obs, vis, nullptr, views, vpart, scratch, buf,
+      ba_eval<false, false, false, false, false, RES, float, NW, PPT, GV && DAVA_PACKED_PAIRS>(L, x, nullptr, 0.f, obs, vis, nullptr, views, vpart, scratch, buf,
                                                      e2, unused);
       if (tid == 0) a.err_out[b] = e2;
     }
