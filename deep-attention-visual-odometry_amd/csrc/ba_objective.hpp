@@ -56,6 +56,10 @@ __device__ unsigned long long g_eval_cycles[kEvalSections];
 // Two points' worth of fp32 in one register pair: the packed pair sweep (PACK) runs the
 // per-(view, point) arithmetic on v_pk_{fma,mul,add}_f32, two points per instruction.
 typedef float pf2 __attribute__((ext_vector_type(2)));
+#ifndef DAVA_PREFETCH_SCENE
+#define DAVA_PREFETCH_SCENE 0  // 1: load the next point pair's observations one step ahead (C5 -7%: registers,
+                               // profiles/r02_ab_prefetch_c5.log)
+#endif
 
 struct Layout {
   int M, N, P, distort;
@@ -546,11 +550,19 @@ __device__ __forceinline__ bool ba_eval(const Layout& L, const S* x, const S* d,
     } else {
       int n0 = tid;
       if constexpr (PACK && RES == DAVA_RESIDUAL_SQUARED_REPROJECTION && std::is_same<S, float>::value) {
-        auto pair2 = [&](int n0, int n1, const pf2 X0, const pf2 X1, const pf2 X2, const pf2 dX0, const pf2 dX1,
-                         const pf2 dX2, pf2& q0, pf2& q1, pf2& q2) {
-          const int i0 = m * N + n0, i1 = m * N + n1;
-          const pf2 obu = {obs[2 * i0], obs[2 * i1]}, obv = {obs[2 * i0 + 1], obs[2 * i1 + 1]};
-          const pf2 wgt = {vis[i0] ? 1.0f : 0.0f, vis[i1] ? 1.0f : 0.0f};
+        // the pair's observations and visibility (read in place from HBM in GV mode); with
+        // DAVA_PREFETCH_SCENE the next pair's are loaded before this pair's arithmetic
+        struct ScenePair {
+          pf2 u, v, w;
+        };
+        auto fetch = [&](int a, int b) {
+          const int i0 = m * N + a, i1 = m * N + b;
+          return ScenePair{pf2{obs[2 * i0], obs[2 * i1]}, pf2{obs[2 * i0 + 1], obs[2 * i1 + 1]},
+                           pf2{vis[i0] ? 1.0f : 0.0f, vis[i1] ? 1.0f : 0.0f}};
+        };
+        auto pair2 = [&](const ScenePair& sp, const pf2 X0, const pf2 X1, const pf2 X2, const pf2 dX0,
+                         const pf2 dX1, const pf2 dX2, pf2& q0, pf2& q1, pf2& q2) {
+          const pf2 obu = sp.u, obv = sp.v, wgt = sp.w;
           auto acc = [](S& a, const pf2 t) {
             a += t.x;
             a += t.y;
@@ -670,8 +682,17 @@ __device__ __forceinline__ bool ba_eval(const Layout& L, const S* x, const S* d,
             }
           }
         };
+        ScenePair next{};
+        if (DAVA_PREFETCH_SCENE && n0 + BLOCK < N) next = fetch(n0, n0 + BLOCK);
         for (; n0 + BLOCK < N; n0 += 2 * BLOCK) {
           const int n1 = n0 + BLOCK, ia = L.pt(n0), ib = L.pt(n1);
+          ScenePair cur;
+          if constexpr (DAVA_PREFETCH_SCENE) {
+            cur = next;
+            if (n0 + 3 * BLOCK < N) next = fetch(n0 + 2 * BLOCK, n0 + 3 * BLOCK);
+          } else {
+            cur = fetch(n0, n1);
+          }
           pf2 X[3], dX[3] = {0.f, 0.f, 0.f}, q[3] = {0.f, 0.f, 0.f};
 #pragma unroll
           for (int c = 0; c < 3; ++c) {
@@ -681,7 +702,7 @@ __device__ __forceinline__ bool ba_eval(const Layout& L, const S* x, const S* d,
               if (m > 0) q[c] = pf2{grad[ia + c], grad[ib + c]};
             }
           }
-          pair2(n0, n1, X[0], X[1], X[2], dX[0], dX[1], dX[2], q[0], q[1], q[2]);
+          pair2(cur, X[0], X[1], X[2], dX[0], dX[1], dX[2], q[0], q[1], q[2]);
           if constexpr (GRAD) {
 #pragma unroll
             for (int c = 0; c < 3; ++c) {
