@@ -303,6 +303,23 @@ def test_c5_shape_global_vector_mode_matches_oracle(device):
         assert (status[:, 0] == 3).all()
 
 
+@pytest.mark.parametrize("xl", [True, False])
+def test_global_vector_packed_sweep_ragged_points_match_oracle(device, xl, monkeypatch):
+    """GV mode's packed pair sweep (two of a thread's points per step) with a ragged point count
+    (1300 points over 512 threads: some threads hold a pair plus a scalar tail, the rest one pair)
+    and Brown-Conrady on, which C5 itself does not exercise; objective on LDS copies (XL) or on
+    the workspace vectors."""
+    x0, obs, vis = _scene(2, 3, 1300, True, 571)
+    kw = dict(iterations=10, error_threshold=-1.0, minimum_step=-1.0)
+    ref = solver.bfgs_solve(x0, objective.ReprojectionClosure(obs, vis, 3, 1300, True), **kw)
+    if not xl:
+        monkeypatch.setenv("DAVA_GV_NO_XL", "1")
+    for mode in ("compact", "dense"):
+        out, status = _gpu_solve(device, x0, obs, vis, 3, 1300, True, hessian_mode=mode, **kw)
+        assert _rel(out, ref).max() <= TOL, (mode, _rel(out, ref))
+        assert (status[:, 0] == 10).all()
+
+
 def test_c5_shape_objective_matches_oracle(device):
     from deep_attention_visual_odometry_amd import native_ops
 
