@@ -432,7 +432,8 @@ __device__ __forceinline__ bool ba_eval(const Layout& L, const S* x, const S* d,
       S G0 = 0.f, G1 = 0.f, G2 = 0.f;  // dE/dp
       S go0 = 0.f, go1 = 0.f;          // dE/d obs (second-order instantiations only)
       if constexpr (RES == DAVA_RESIDUAL_SQUARED_REPROJECTION) {
-        // projection
+        // projection; the distorted model nudges z' == 0 by 1e-8 (distorted_camera_model.py:57)
+        if (L.distort && p2 == S(0.0f)) p2 = p2 + 1e-8f;
         const S iz = 1.0f / p2;
         const S qx = p0 * iz, qy = p1 * iz;
         const S ub = in.f * qx, vb = in.f * qy;
@@ -599,6 +600,10 @@ __device__ __forceinline__ bool ba_eval(const Layout& L, const S* x, const S* d,
               dp1 = da1 * vc + a1 * dc + k * w1 + Avw * dw1 + e1 * vB + c1 * dB + dtt1;
               dp2 = da2 * vc + a2 * dc + k * w2 + Avw * dw2 + e2 * vB + c2 * dB + dtt2;
             }
+          }
+          if (L.distort) {  // z' == 0 nudge (distorted_camera_model.py:57)
+            if (p2.x == 0.0f) p2.x += 1e-8f;
+            if (p2.y == 0.0f) p2.y += 1e-8f;
           }
           const pf2 iz = 1.0f / p2;
           const pf2 qx = p0 * iz, qy = p1 * iz;

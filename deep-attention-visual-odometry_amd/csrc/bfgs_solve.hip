@@ -176,6 +176,12 @@ __device__ __forceinline__ void st4(float* p, float4 v) { *reinterpret_cast<floa
 #ifndef DAVA_TRIAL_CHECK
 #define DAVA_TRIAL_CHECK 1  // skip evaluating trial points that round back to x
 #endif
+#ifndef DAVA_DEBUG_TRIALS
+#define DAVA_DEBUG_TRIALS -1  // diagnostic builds: >= 0 prints that problem's line-search trials
+#endif
+#ifndef DAVA_NONFINITE_DOT
+#define DAVA_NONFINITE_DOT 1  // overflowed trials: slope re-formed as grad . d (the reference's class)
+#endif
 #ifndef DAVA_FUSED_PAIR
 #define DAVA_FUSED_PAIR 1  // two history entries in flight per wave (0: one; fewer VGPRs)
 #endif
@@ -1181,6 +1187,23 @@ __global__ __launch_bounds__(kWave * NW, DAVA_SOLVE_WAVES_PER_EU) void bfgs_ba_s
                 L, x, d, al, obs, vis, grad_buf(gp), views, vpart, scratch, buf, fa, dfa)) {
           ++evals;
           last_same = false;
+#if DAVA_NONFINITE_DOT
+          // Overflowed trial (fp32 at a wild step): the reference's phi'(alpha) is autograd w.r.t.
+          // alpha, i.e. (grad E(x + alpha d) * d).sum() (wolfe_conditions.py:134-143) -- NaN as
+          // soon as the reverse-mode gradient holds a NaN or infinities of both signs, where the
+          // forward-mode tangent may come out as +-Inf.  The NaN-blind Wolfe comparisons branch on
+          // that class (a -Inf slope passes `phi' (a_hi - a_lo) >= 0` when a_hi < a_lo, NaN does
+          // not), so here the slope is re-formed from the trial's reverse-mode gradient.  Finite
+          // trials keep the forward-mode slope bit for bit.  Uniform branch (fa, dfa are
+          // block-reduced); ba_eval<GRAD> ends with a barrier, so the gradient is complete.
+          if (!(isfinite(fa) && isfinite(dfa))) {
+            const float* gt = grad_buf(gp);
+            float r[1] = {0.f};
+            for (int i = tid; i < P; i += BLOCK) r[0] += gt[i] * d[i];
+            block_sum<1, NW>(r, scratch, buf); buf ^= 1;
+            dfa = r[0];
+          }
+#endif
         } else {
           fa = E;
           dfa = dphi0;
@@ -1188,6 +1211,12 @@ __global__ __launch_bounds__(kWave * NW, DAVA_SOLVE_WAVES_PER_EU) void bfgs_ba_s
           if (!known_same) nomove_al = al;
         }
         DAVA_PHASE(3);
+#if DAVA_DEBUG_TRIALS >= 0
+        // diagnostic builds only (make variant FLAGS=-DDAVA_DEBUG_TRIALS=<problem>): every trial
+        if (b == DAVA_DEBUG_TRIALS && tid == 0)
+          printf("TRIAL k=%d t=%d alpha=%.9g f=%.9g dphi=%.9g f0=%.9g dphi0=%.9g lo=%.9g hi=%.9g zoom=%d\n", k, t, al,
+                 fa, dfa, E, dphi0, a_lo, a_hi, (int)zoom);
+#endif
         ++trials;
         evaluated = true;
         last_al = al;

@@ -254,8 +254,19 @@ def ba_solve_backward(x_out_grad: Tensor, tape: Tensor, status: Tensor, observat
     b, dev = x_out_grad.shape[0], x_out_grad.device
     if tuple(status.shape) != (b, N.STATUS_WORDS) or status.dtype != torch.int32 or not status.is_contiguous():
         raise ValueError("status must be the recording call's contiguous (B, 4) int32 tensor")
+    # the kernel dereferences tape and status as device memory of this launch: refuse anything else
+    # loudly rather than fault the GPU (a CPU or other-device tensor, a short or strided tape)
+    for what, t in (("tape", tape), ("status", status)):
+        if t.device != dev:
+            raise ValueError(f"{what} must be on {dev} (the cotangent's device), got {t.device}")
+    if tape.dtype != torch.uint8 or tape.dim() != 1 or not tape.is_contiguous():
+        raise ValueError("tape must be the recording call's contiguous 1-D uint8 tensor")
     sc = scene_struct(observations, visibility, num_views, num_points, distortion, b, residual)
     cfg = solver_config(1e-4, 0.9, 1e-4, iterations, 1e-8, 1000, True, N.DAVA_HESSIAN_COMPACT)
+    tape_need = int(lib.dava_ba_solve_tape_bytes(sc, cfg))
+    if tape.numel() < tape_need:
+        raise ValueError(f"tape holds {tape.numel()} bytes; a recording of this scene and iteration count "
+                         f"writes {tape_need}")
     need = int(lib.dava_ba_solve_backward_workspace_bytes(sc, cfg))
     if need == 0:
         raise ValueError("this scene / configuration has no fused adjoint")

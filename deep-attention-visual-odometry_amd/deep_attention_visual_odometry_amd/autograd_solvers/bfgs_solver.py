@@ -101,7 +101,30 @@ class BFGSSolver(Module):
             if self._adjoint_available(parameters, error_function, num_iterations):
                 return self._fused_differentiable(parameters, error_function, error_threshold, num_iterations,
                                                   drop_p, seed)
+        if isinstance(error_function, ReprojectionError):
+            self._check_generic_fits(parameters, num_iterations)
         return self._generic(parameters, error_function, error_threshold, num_iterations)
+
+    def _check_generic_fits(self, parameters, num_iterations) -> None:
+        """A fused objective that the fused kernels cannot take (differentiating a GV-mode solve,
+        P > 1024; dense mode or more than 1025 iterations with a graph; training mode's
+        return_second_last) runs the generic loop, which holds the reference's dense (B, P, P)
+        inverse Hessian -- and, with a graph, about three P x P tensors per problem per iteration.
+        Where that cannot fit the device, refuse up front instead of running out of memory midway."""
+        lead = parameters.shape[:-1]
+        b = max(int(torch.tensor(lead).prod().item()) if len(lead) else 1, 1)
+        p = parameters.size(-1)
+        per_matrix = b * p * p * parameters.element_size()
+        need = per_matrix * (3 * num_iterations + 2 if parameters.requires_grad else 8)
+        free, _ = torch.cuda.mem_get_info(parameters.device)
+        if need > free:
+            what = ("differentiating through the solve" if parameters.requires_grad
+                    else "training mode with return_second_last")
+            raise RuntimeError(
+                f"{what} at B={b}, P={p}, {num_iterations} iterations has no fused kernel here (the adjoint covers "
+                f"compact mode with P <= 1024 and at most {self.MAX_COMPACT_ENTRIES + 1} iterations); the generic "
+                f"loop would hold the dense (B, P, P) inverse Hessian ~{need / 2 ** 30:.0f} GiB against "
+                f"{free / 2 ** 30:.0f} GiB free. Reduce the batch or the iteration count.")
 
     def _adjoint_available(self, parameters, fn: ReprojectionError, num_iterations) -> bool:
         """Differentiating through a fused objective's solve runs the recording solve + adjoint

@@ -16,9 +16,11 @@ where pi_m is:
      that it broadcasts correctly for batch > 1),
   2. p = X/s for view 0, p = R(w_m) X/s + t_m/s for views m >= 1
      (``:107-115``, Rodrigues from ``geometry/axis_angle_rotation.py:25-48``),
-  3. u = f*x/z + cx, v = f*y/z + cy (``geometry/camera_projection.py:20-35``),
-     optionally followed by the Brown-Conrady block of
-     ``camera_model/distorted_camera_model.py:59-86`` with fx = fy = f, s = 0.
+  3. u = f*x/z + cx, v = f*y/z + cy (``geometry/camera_projection.py:20-35``), or with
+     distortion the reference's own distorted model (``camera_model/distorted_camera_model.py:
+     24-103``: z' nudge, u = fx (x/z) + s (y/z), v = fy (y/z), radial + tangential block) on
+     camera rows fx = fy = f, s = 0, zero rotation / translation -- pinned bitwise to that
+     file's output (``tests/golden/distortion.npz``).
 
 Every op is written in the same order as the reference so that fp64/fp32
 values and autograd gradients round identically.
@@ -82,27 +84,54 @@ def view_points(points: torch.Tensor, translations: torch.Tensor, rotations: tor
     return torch.concatenate([points, moved], dim=-3)
 
 
-def project(p: torch.Tensor, intrinsics: torch.Tensor, distortion: Optional[torch.Tensor]) -> torch.Tensor:
-    """Pinhole (``geometry/camera_projection.py:20-35``) plus optional
-    Brown-Conrady on the f-scaled coordinates (``distorted_camera_model.py:59-86``)."""
-    f = intrinsics[..., 0:1]
-    c = intrinsics[..., 1:3]
-    if distortion is None:
-        return f * p[..., 0:2] / p[..., 2:3] + c
-    z = p[..., 2:3]
-    u = f * p[..., 0:1] / z
-    v = f * p[..., 1:2] / z
-    k1 = distortion[..., 0:1]
-    k2 = distortion[..., 1:2]
-    k3 = distortion[..., 2:3]
-    p1 = distortion[..., 3:4]
-    p2 = distortion[..., 4:5]
+def project(p: torch.Tensor, intrinsics: torch.Tensor) -> torch.Tensor:
+    """Pinhole (``geometry/camera_projection.py:20-35``): f * xy / z + c."""
+    return intrinsics[..., 0:1] * p[..., 0:2] / p[..., 2:3] + intrinsics[..., 1:3]
+
+
+# slot order of the reference's 16-parameter camera table (``spatial_maths.camera_model_parameters``,
+# as listed by ``tests/camera_model/test_distorted_camera_model.py:13-30``)
+CX, CY, K1, K2, K3, P1, P2, FX, SKEW, FY = range(10)
+
+
+def camera_rows(x: torch.Tensor, num_views: int) -> torch.Tensor:
+    """(B, P) BA parameters -> (B*M, 16) camera rows in the reference's slot order: fx = fy = f,
+    skew, rotation and translation 0 (the BA objective supplies camera-relative points),
+    cx, cy, k1 k2 k3 p1 p2 from x (distortion = the last 5 entries)."""
+    b = x.shape[0]
+    zero = x.new_zeros(b, 1)
+    f, cx, cy, k = x[:, 0:1], x[:, 1:2], x[:, 2:3], x[:, -5:]
+    row = torch.cat([cx, cy, k, f, zero, f] + [zero] * 6, dim=-1)
+    return row[:, None, :].expand(b, num_views, 16).reshape(b * num_views, 16)
+
+
+def distorted_rows(pts: torch.Tensor, rows: torch.Tensor):
+    """u', v' (R, N) of points (R, N, 3) under camera rows (R, 16): the reference's
+    ``_full_forward_model`` (``camera_model/distorted_camera_model.py:24-103``) at zero rotation
+    and translation -- its extrinsic step is then the identity, bit for bit -- with the z' == 0
+    nudge (:57), the f-scaled coordinates u = fx (x'/z') + s (y'/z'), v = fy (y'/z') (:59-62)
+    and the radial / tangential block (:64-86), in the same operation order."""
+    xp = pts[:, :, 0]
+    yp = pts[:, :, 1]
+    zp = pts[:, :, 2].clone()
+    zp[zp == 0] += 1e-8
+    u = rows[:, None, FX] * (xp / zp) + rows[:, None, SKEW] * (yp / zp)
+    v = rows[:, None, FY] * (yp / zp)
     r2 = u * u + v * v
     uv = u * v
-    radial = 1.0 + k1 * r2 + k2 * r2 * r2 + k3 * r2 * r2 * r2
-    ud = u * radial + 2.0 * p1 * uv + p2 * (r2 + 2 * u * u) + c[..., 0:1]
-    vd = v * radial + 2.0 * p2 * uv + p1 * (r2 + 2 * v * v) + c[..., 1:2]
-    return torch.cat([ud, vd], dim=-1)
+    radial = (1.0 + rows[:, None, K1] * r2 + rows[:, None, K2] * r2 * r2
+              + rows[:, None, K3] * r2 * r2 * r2)
+    ud = u * radial + 2.0 * rows[:, None, P1] * uv + rows[:, None, P2] * (r2 + 2 * u * u) + rows[:, None, CX]
+    vd = v * radial + 2.0 * rows[:, None, P2] * uv + rows[:, None, P1] * (r2 + 2 * v * v) + rows[:, None, CY]
+    return ud, vd
+
+
+def project_distorted(p: torch.Tensor, x: torch.Tensor, num_views: int) -> torch.Tensor:
+    """Brown-Conrady projection of camera-relative points p (B, M, N, 3) for BA parameters x
+    (B, P): ``distorted_rows`` per view on (B*M, N) rows, as the reference model evaluates them."""
+    b, _, n, _ = p.shape
+    ud, vd = distorted_rows(p.reshape(b * num_views, n, 3), camera_rows(x, num_views))
+    return torch.stack([ud, vd], dim=-1).reshape(b, num_views, n, 2)
 
 
 def reprojection_error(
@@ -116,7 +145,12 @@ def reprojection_error(
     """E(x), shape x.shape[:-1].  observations (..., M, N, 2), visibility (..., M, N)."""
     parts = split_parameters(x, num_views, num_points, distortion)
     p = view_points(parts.points, parts.translations, parts.rotations)
-    uv = project(p, parts.intrinsics, parts.distortion)
+    lead = x.shape[:-1]
+    if distortion:
+        uv = project_distorted(p.reshape((-1,) + p.shape[-3:]), x.reshape(-1, x.size(-1)), num_views)
+        uv = uv.reshape(lead + uv.shape[-3:])
+    else:
+        uv = project(p, parts.intrinsics)
     sq = (uv - observations).square().sum(dim=-1)
     return (sq * visibility.to(sq.dtype)).sum(dim=(-1, -2))
 

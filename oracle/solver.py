@@ -59,8 +59,11 @@ def wolfe_line_search(
     c2: float = 0.9,
     strong: bool = False,
     trials: Optional[list] = None,
+    trial_log: Optional[list] = None,
 ) -> torch.Tensor:
-    """Returns alpha (shape x.shape[:-1]); see module docstring."""
+    """Returns alpha (shape x.shape[:-1]); see module docstring.  ``trial_log`` (diagnostics)
+    receives one dict per call: the base point, direction, f0, phi'(0) and, per trial, the
+    active mask, alpha, f(alpha) and phi'(alpha)."""
     x = x.detach()
     direction = direction.detach()
     f0 = f0.detach()
@@ -78,6 +81,10 @@ def wolfe_line_search(
     f_hi = f0.clone()
     f_a = f0.clone()
     dphi_a = dphi0.clone()
+    log = None
+    if trial_log is not None:
+        log = dict(x=x.clone(), direction=direction.clone(), f0=f0.clone(), dphi0=dphi0.clone(), trials=[])
+        trial_log.append(log)
     for trial in range(1000):
         active = widen | zoom
         if not active.any():
@@ -95,6 +102,8 @@ def wolfe_line_search(
             (dfa,) = torch.autograd.grad(fa.sum(), alpha)
         f_a[active] = fa.detach()
         dphi_a[active] = dfa.squeeze(-1).detach()
+        if log is not None:
+            log["trials"].append(dict(active=active.clone(), alpha=a.clone(), f=f_a.clone(), dphi=dphi_a.clone()))
 
         sufficient_fail[active] = f_a[active] > f0[active] + c1 * a[active] * dphi0[active]
         sufficient_fail[zoom] |= f_a[zoom] >= f_lo[zoom]
@@ -158,6 +167,7 @@ def bfgs_solve(
     minimum_step: float = 1e-8,
     record: Optional[SolveRecord] = None,
     trajectory: Optional[list] = None,
+    trial_log: Optional[list] = None,
     training: bool = False,
     drop_path_p: float = 0.0,
     return_second_last: bool = False,
@@ -226,7 +236,7 @@ def bfgs_solve(
             h = h.masked_scatter(active.unsqueeze(-1).unsqueeze(-1).expand_as(h), ha)
         alpha = wolfe_line_search(
             xa, d, fa, ga, sub_closure, c1, c2, strong=True,
-            trials=None if record is None else record.line_search_trials,
+            trials=None if record is None else record.line_search_trials, trial_log=trial_log,
         )
         s = alpha.unsqueeze(-1) * d
         step = step.masked_scatter(active.unsqueeze(-1).expand_as(step), s)

@@ -50,6 +50,12 @@ Fixtures written:
                           default -1, points pushed behind the camera, hidden pairs), and
                           BFGSCameraSolver + LineSearchStrongWolfeConditions results with the
                           bfgs_solver_*_config.yaml settings (fp64).
+* ``distortion.npz``  -- Brown-Conrady pinned to the reference's own ``_full_forward_model``
+                          (distorted_camera_model.py:24-103, loaded by path with the 16-slot
+                          index table its test lists): the projection alone (u', v' and
+                          autograd), the BA objective with the distorted model (C1/C2/C3
+                          shapes, fp32/fp64) and BFGSSolver().eval() on it after K = 5/20/100
+                          at the headline shape (C3 + Brown-Conrady, fp32).
 * ``bfgs_traj.npz``   -- ``BFGSSolver(...).eval()`` results after K in
                           {5, 20, 100} iterations (error_threshold = -1,
                           minimum_step = -1) for C1 (2x64), C2 (2x128) and
@@ -557,9 +563,133 @@ def gen_camera_l1_autograd():
     np.savez_compressed(os.path.join(HERE, "camera_l1_autograd.npz"), **out)
 
 
+# ---- Brown-Conrady, pinned to the reference's own forward model ----------------------------------
+
+# distorted_camera_model.py:3 imports ``spatial_maths.camera_model_parameters`` (absent: not on any
+# index this image has) for 16 slot indices.  The reference's own test lists the slot order
+# (tests/camera_model/test_distorted_camera_model.py:13-30); the module is only that table, so it is
+# supplied in THIS process as data, and the reference file itself is loaded by path, unmodified.
+BC_SLOTS = ["CX", "CY", "K1", "K2", "K3", "P1", "P2", "FX", "S", "FY", "RX", "RY", "RZ", "TX", "TY", "TZ"]
+
+
+def reference_distorted_model(scripted: bool = True):
+    """The reference file loaded by path.  scripted=False runs its functions eagerly (the
+    ``@torch.jit.script`` decorator as the identity, what PYTORCH_JIT=0 does): the forward values
+    are the same bits, but TorchScript's executor differentiates with its own symbolic backward
+    (and the first, profiling call differently from later ones), so eager mode is the one
+    reproducible reference for the gradients."""
+    import importlib.util
+    import types
+    from unittest import mock
+
+    if "spatial_maths.camera_model_parameters" not in sys.modules:
+        pkg = types.ModuleType("spatial_maths")
+        pkg.__path__ = []
+        table = types.ModuleType("spatial_maths.camera_model_parameters")
+        for i, name in enumerate(BC_SLOTS):
+            setattr(table, name, i)
+        pkg.camera_model_parameters = table
+        sys.modules["spatial_maths"] = pkg
+        sys.modules["spatial_maths.camera_model_parameters"] = table
+    path = "/root/reference/deep_attention_visual_odometry/camera_model/distorted_camera_model.py"
+    spec = importlib.util.spec_from_file_location(f"reference_distorted_camera_model_{int(scripted)}", path)
+    mod = importlib.util.module_from_spec(spec)
+    if scripted:
+        spec.loader.exec_module(mod)
+    else:
+        with mock.patch.object(torch.jit, "script", lambda fn: fn):
+            spec.loader.exec_module(mod)
+    return mod
+
+
+def bc_parameters(x, m):
+    """(B, P) BA parameters -> (B*M, 16) rows of the reference's slot table: fx = fy = f, skew 0,
+    rotation and translation 0 (the BA objective supplies camera-relative points), cx, cy and
+    k1 k2 k3 p1 p2 from x (the distortion block is the last 5 entries of x)."""
+    b = x.shape[0]
+    zero = x.new_zeros(b, 1)
+    f, cx, cy, k = x[:, 0:1], x[:, 1:2], x[:, 2:3], x[:, -5:]
+    row = torch.cat([cx, cy, k, f, zero, f, zero, zero, zero, zero, zero, zero], dim=-1)
+    return row[:, None, :].expand(b, m, 16).reshape(b * m, 16)
+
+
+def ref_objective_bc(x, obs, vis, m, n, model):
+    """The BA objective with the reference's distorted camera model (_full_forward_model,
+    distorted_camera_model.py:24-103) in place of the plain pinhole: unpack (without the 5
+    coefficients) -> camera-relative points -> per-view distorted projection -> squared residual."""
+    parts = unpack_calibration_parameters(x[..., :-5], m, n)
+    rel = ref_relative_points(parts.world_points, parts.camera_translations, parts.camera_rotations, x.shape[0])
+    out = model._full_forward_model(rel.reshape(-1, n, 3), bc_parameters(x, m))
+    uv = torch.stack([out.u_prime, out.v_prime], dim=-1).reshape(x.shape[0], m, n, 2)
+    sq = (uv - obs).square().sum(dim=-1)
+    return (sq * vis.to(sq.dtype)).sum(dim=(-1, -2))
+
+
+def gen_distortion():
+    """Eager-mode reference (bitwise target of the oracle) plus, for the projection and the
+    objective, the TorchScript-mode gradients (second call, the executor's optimised graph) and the
+    TorchScript-mode trajectory, to show how far the reference's own two executors lie apart."""
+    eager, scripted = reference_distorted_model(False), reference_distorted_model(True)
+    out = {}
+    rng = np.random.default_rng(9500)
+    # 1. the projection alone: camera-relative points, (B, 16) parameters in the BA's tie
+    #    (fx = fy, s = R = T = 0); u', v' and autograd of a random-weighted sum w.r.t. both inputs
+    for dt_name, dt in (("f64", torch.float64), ("f32", torch.float32)):
+        b, n = 3, 64
+        pts = rng.normal(0.0, 1.0, size=(b, n, 3)) * np.array([3.0, 3.0, 1.0]) + np.array([0.0, 0.0, 20.0])
+        if dt_name == "f64":
+            pts[2, 5, 2] = 0.0  # z' == 0: the model's nudge (distorted_camera_model.py:57)
+        f = 1.0 / np.tan(rng.uniform(np.pi / 6, 2 * np.pi / 3, size=b) / 2.0)
+        x = np.zeros((b, 3 + 5))
+        x[:, 0], x[:, 1:3] = f, rng.normal(0.0, 0.2, size=(b, 2))
+        x[:, 3:] = rng.normal(size=(b, 5)) * np.array([1e-2, 1e-3, 1e-4, 1e-3, 1e-3])
+        wu = torch.tensor(rng.normal(size=(b, n)), dtype=dt)
+        wv = torch.tensor(rng.normal(size=(b, n)), dtype=dt)
+        key = f"proj_{dt_name}"
+        for tag, model, calls in (("", eager, 1), ("_jit", scripted, 2)):
+            for _ in range(calls):  # TorchScript: the second call runs the optimised graph
+                xt = torch.tensor(x, dtype=dt, requires_grad=True)
+                p = torch.tensor(pts, dtype=dt, requires_grad=True)
+                res = model._full_forward_model(p, bc_parameters(xt, 1))
+                gp, gx = torch.autograd.grad((res.u_prime * wu).sum() + (res.v_prime * wv).sum(), [p, xt])
+            out[key + tag + "_u"], out[key + tag + "_v"] = res.u_prime.detach().numpy(), res.v_prime.detach().numpy()
+            out[key + tag + "_grad_points"], out[key + tag + "_grad_x"] = gp.numpy(), gx.numpy()
+        out[key + "_points"], out[key + "_x"] = p.detach().numpy(), xt.detach().numpy()
+        out[key + "_wu"], out[key + "_wv"] = wu.numpy(), wv.numpy()
+    # 2. the whole BA objective with the distorted model, B = 1 (the reference's own
+    #    get_camera_relative_points), error and autograd gradient
+    for name, (m, n) in SHAPES.items():
+        for dt_name, dt in (("f64", torch.float64), ("f32", torch.float32)):
+            s = make_scenes(1, m, n, distortion=True, seed=7501)
+            obs, vis = torch.tensor(s.observations, dtype=dt), torch.tensor(s.visibility)
+            key = f"eval_{name}_{dt_name}"
+            for tag, model, calls in (("", eager, 1), ("_jit", scripted, 2)):
+                for _ in range(calls):
+                    x = torch.tensor(s.initial, dtype=dt, requires_grad=True)
+                    e = ref_objective_bc(x, obs, vis, m, n, model)
+                    (g,) = torch.autograd.grad(e.sum(), x)
+                out[key + tag + "_err"], out[key + tag + "_grad"] = e.detach().numpy(), g.numpy()
+            out[key + "_x"], out[key + "_obs"], out[key + "_vis"] = x.detach().numpy(), obs.numpy(), vis.numpy()
+    # 3. BFGSSolver().eval() on it: the headline model (C3 + Brown-Conrady, fp32) after K = 5, 20, 100
+    m, n = SHAPES["c3"]
+    s = make_scenes(4, m, n, distortion=True, seed=7502)
+    x0, obs, vis = torch.tensor(s.initial), torch.tensor(s.observations), torch.tensor(s.visibility)
+    out["traj_c3_x0"], out["traj_c3_obs"], out["traj_c3_vis"] = x0.numpy(), obs.numpy(), vis.numpy()
+    for tag, model in (("", eager), ("_jit", scripted)):
+        def fn(x, mask, model=model):
+            return ref_objective_bc(x, obs[mask], vis[mask], m, n, model)
+
+        for k in (5, 20, 100):
+            solver = BFGSSolver(iterations=k, error_threshold=-1.0, minimum_step=-1.0).eval()
+            out[f"traj_c3{tag}_k{k}"] = solver(x0, fn).numpy()
+    np.savez_compressed(os.path.join(HERE, "distortion.npz"), **out)
+
+
 if __name__ == "__main__":
     torch.set_num_threads(8)
-    which = sys.argv[1:] or ["eval", "update", "ls", "traj", "ray", "grad", "train", "l1", "l1grad"]
+    which = sys.argv[1:] or ["eval", "update", "ls", "traj", "ray", "grad", "train", "l1", "l1grad", "bc"]
+    if "bc" in which:
+        gen_distortion()
     if "eval" in which:
         gen_ba_eval()
     if "update" in which:

@@ -91,6 +91,43 @@ def test_golden_reference_evaluation(device, shape):
     assert ((grad.cpu().double() - g_ref).norm() / g_ref.norm()).item() < 1e-4
 
 
+@pytest.mark.parametrize("shape", list(SHAPES))
+def test_golden_reference_distorted_evaluation(device, shape):
+    """Brown-Conrady against the REFERENCE's own distorted model (tests/golden/distortion.npz:
+    distorted_camera_model.py's _full_forward_model composed into the BA objective): the kernel's
+    fp32 error and gradient vs the reference's fp64 values on the same inputs."""
+    from deep_attention_visual_odometry_amd import native_ops
+
+    g = np.load(os.path.join(GOLDEN, "distortion.npz"))
+    m, n = SHAPES[shape]
+    key = f"eval_{shape}_f32"
+    x = torch.tensor(g[key + "_x"])
+    e, grad, _ = native_ops.ba_evaluate(x.to(device), torch.tensor(g[key + "_obs"]).to(device),
+                                        torch.tensor(g[key + "_vis"]).to(device), m, n, True)
+    e_ref = torch.tensor(g[f"eval_{shape}_f64_err"])
+    g_ref = torch.tensor(g[f"eval_{shape}_f64_grad"])
+    assert torch.allclose(e.cpu().double(), e_ref, rtol=2e-5)
+    assert ((grad.cpu().double() - g_ref).norm() / g_ref.norm()).item() < 1e-4
+    # the distortion block's own gradient (5 entries, small next to the point coordinates')
+    assert ((grad.cpu().double()[:, -5:] - g_ref[:, -5:]).norm() / g_ref[:, -5:].norm()).item() < 1e-4
+
+
+def test_distorted_model_z_nudge(device):
+    """A camera-relative point exactly on z' = 0: the distorted model nudges z' by 1e-8
+    (distorted_camera_model.py:57), as the oracle (pinned to that file) does -- both give the
+    same (finite or not) class of error, and the same value where it is finite."""
+    from deep_attention_visual_odometry_amd import native_ops
+
+    x, obs, vis = _scene(1, 2, 64, True, 17)
+    x[0, 3 + 3 * 5 + 2] = 0.0  # view 0 sees point 5 at z = 0 (view 0 is the identity camera)
+    x[0, -5:] = 0.0  # no distortion: u = f x / 1e-8 stays finite in fp32 squared ... or overflows alike
+    e, _, _ = native_ops.ba_evaluate(x.to(device), obs.to(device), vis.to(device), 2, 64, True, want_grad=False)
+    e_ref = objective.reprojection_error(x, obs, vis, 2, 64, True)
+    assert torch.isfinite(e.cpu()).all() == torch.isfinite(e_ref).all()
+    if torch.isfinite(e_ref).all():
+        assert torch.allclose(e.cpu().double(), e_ref.double(), rtol=1e-5)
+
+
 def test_slope_is_directional_derivative_of_gradient(device):
     """phi'(alpha) from forward mode == d . grad from reverse mode, same kernel."""
     from deep_attention_visual_odometry_amd import native_ops

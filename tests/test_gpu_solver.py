@@ -54,17 +54,22 @@ def _rel(a, b):
     return rel
 
 
-def _envelopes(x0, fn, ref, **kw):
+def _envelopes(x0, fn, ref, distortion=False, **kw):
     """Per-problem 10x the oracle's own change under a 1-ulp nudge of x0, up or down (floor
-    1e-5), for the whole parameter vector and for the intrinsics alone.  Both directions: which
-    side of a bifurcation a nudge lands on depends on the host CPU's torch kernels."""
-    env, env_i = torch.full((x0.shape[0],), TOL, dtype=torch.float64), torch.full((x0.shape[0],), TOL,
-                                                                                     dtype=torch.float64)
+    1e-5), for the whole parameter vector, for the intrinsics alone and (distortion) for the five
+    Brown-Conrady coefficients alone.  Both directions: which side of a bifurcation a nudge lands
+    on depends on the host CPU's torch kernels.  The distortion block is the least determined
+    part of x (k1..p2 are still 10-100% from the truth at K = 100): the reference's own 1-ulp
+    spread on it is 1e-4 .. 4e-3 at the headline shape, against ~5e-7 for the whole vector."""
+    b = x0.shape[0]
+    env, env_i, env_d = (torch.full((b,), TOL, dtype=torch.float64) for _ in range(3))
     for to in (float("inf"), -float("inf")):
         nudged = solver.bfgs_solve(torch.nextafter(x0, torch.full_like(x0, to)), fn, **kw)
         env = torch.maximum(env, 10.0 * _rel(nudged, ref))
         env_i = torch.maximum(env_i, 10.0 * _rel(nudged[:, :3], ref[:, :3]))
-    return env, env_i
+        if distortion:
+            env_d = torch.maximum(env_d, 10.0 * _rel(nudged[:, -5:], ref[:, -5:]))
+    return (env, env_i, env_d) if distortion else (env, env_i)
 
 
 def _report(tag, rel, env=None, extra=None):
@@ -185,17 +190,18 @@ def _headline_reference():
         fn = objective.ReprojectionClosure(obs, vis, 4, 256, True)
         kw = dict(iterations=100, error_threshold=-1.0, minimum_step=-1.0)
         ref = solver.bfgs_solve(x0, fn, **kw)
-        env, env_i = _envelopes(x0, fn, ref, **kw)
-        _HEADLINE.update(x0=x0, obs=obs, vis=vis, ref=ref, env=env, env_i=env_i)
+        env, env_i, env_d = _envelopes(x0, fn, ref, distortion=True, **kw)
+        _HEADLINE.update(x0=x0, obs=obs, vis=vis, ref=ref, env=env, env_i=env_i, env_d=env_d)
     return _HEADLINE
 
 
 @pytest.mark.parametrize("mode", ["compact", "dense"])
 def test_headline_workload_matches_oracle(device, mode):
     """Parity AT the benchmarked configuration (C3 + Brown-Conrady, P = 794, K = 100, both
-    inverse-Hessian modes), on the bench's own problems, against the oracle.  Brown-Conrady is
-    parity-unpinned against reference outputs (its module imports the absent spatial_maths): the
-    oracle restates distorted_camera_model.py:59-86.  The full distribution is reported."""
+    inverse-Hessian modes), on the bench's own problems, against the oracle -- per block: the whole
+    vector, the intrinsics (f, cx, cy) and the five distortion coefficients, each inside the
+    reference's own 1-ulp envelope for that block.  The oracle's Brown-Conrady path is pinned
+    bitwise to the reference's distorted model (tests/golden/distortion.npz)."""
     h = _headline_reference()
     out, status = _gpu_solve(device, h["x0"], h["obs"], h["vis"], 4, 256, True, iterations=100,
                              error_threshold=-1.0, minimum_step=-1.0, hessian_mode=mode)
@@ -203,11 +209,46 @@ def test_headline_workload_matches_oracle(device, mode):
     rel_i = _rel(out[:, :3], h["ref"][:, :3])
     rel_d = _rel(out[:, -5:], h["ref"][:, -5:])
     _report(f"headline_{mode}_C3_BC_K100_B16", rel, h["env"],
-            {"intrinsics_max_rel": float(rel_i.max()), "distortion_max_rel": float(rel_d.max())})
+            {"intrinsics_max_rel": float(rel_i.max()), "distortion_max_rel": float(rel_d.max()),
+             "distortion_envelope_min": float(h["env_d"].min()), "distortion_envelope_max": float(h["env_d"].max()),
+             "distortion_n_outside_envelope": int((rel_d > h["env_d"]).sum()),
+             "distortion_max_rel_over_envelope": float((rel_d / h["env_d"]).max())})
     assert (status[:, 0] == 100).all()
     assert (rel <= h["env"]).all(), rel
-    assert (rel <= TOL).double().mean() >= 0.9, rel
+    assert (rel <= TOL).all(), rel
     assert (rel_i <= h["env_i"]).all(), rel_i
+    assert (rel_d <= h["env_d"]).all(), (rel_d, h["env_d"])
+
+
+@pytest.mark.parametrize("mode", ["compact", "dense"])
+def test_reference_golden_distorted_trajectories(device, mode):
+    """Against BFGSSolver().eval() of the REAL reference on the headline model -- the BA objective
+    with the reference's own distorted camera model (tests/golden/distortion.npz, C3 + Brown-Conrady,
+    fp32) -- after K = 5, 20 (1e-5) and 100 (per block, inside the reference's 1-ulp envelopes).
+    The reference's two executors (eager / TorchScript) differ on k1..p2 by up to ~1e-3 at K = 100."""
+    g = np.load(os.path.join(GOLDEN, "distortion.npz"))
+    x0 = torch.tensor(g["traj_c3_x0"])
+    obs, vis = torch.tensor(g["traj_c3_obs"]), torch.tensor(g["traj_c3_vis"])
+    fn = objective.ReprojectionClosure(obs, vis, 4, 256, True)
+    for k in (5, 20, 100):
+        out, status = _gpu_solve(device, x0, obs, vis, 4, 256, True, iterations=k, error_threshold=-1.0,
+                                 minimum_step=-1.0, hessian_mode=mode)
+        ref = torch.tensor(g[f"traj_c3_k{k}"])
+        rel, rel_d = _rel(out, ref), _rel(out[:, -5:], ref[:, -5:])
+        jit_d = _rel(torch.tensor(g[f"traj_c3_jit_k{k}"])[:, -5:], ref[:, -5:])
+        assert (status[:, 0] == k).all()
+        if k <= 20:
+            _report(f"golden_bc_{mode}_c3_K{k}", rel, None, {"distortion_max_rel": float(rel_d.max())})
+            assert rel.max() <= TOL, (k, rel)
+            continue
+        kw = dict(iterations=k, error_threshold=-1.0, minimum_step=-1.0)
+        env, env_i, env_d = _envelopes(x0, fn, ref, distortion=True, **kw)
+        _report(f"golden_bc_{mode}_c3_K{k}", rel, env,
+                {"distortion_max_rel": float(rel_d.max()), "distortion_envelope_max": float(env_d.max()),
+                 "reference_eager_vs_torchscript_distortion_max_rel": float(jit_d.max())})
+        assert (rel <= env).all() and (rel <= TOL).all(), rel
+        assert (_rel(out[:, :3], ref[:, :3]) <= env_i).all()
+        assert (rel_d <= env_d).all(), (rel_d, env_d)
 
 
 def test_default_stopping_rules(device):
@@ -605,3 +646,17 @@ def test_fused_drop_path_is_the_eval_solve_stopped_early(device):
                                         iterations=int(steps), error_threshold=-1.0, minimum_step=-1.0,
                                         hessian_mode=1)
         assert torch.equal(out[idx], ref.cpu()), steps
+
+
+def test_infeasible_generic_fallback_raises(device):
+    """Differentiating a GV-mode (C5-shaped) solve has no fused adjoint; the generic loop would hold
+    the dense (B, P, P) inverse Hessian per iteration in the graph (hundreds of GiB): refused up
+    front with a RuntimeError, never attempted."""
+    from deep_attention_visual_odometry_amd import BFGSSolver, ReprojectionError
+
+    m, n = 16, 4096
+    p = 3 + 3 * n + 6 * (m - 1)
+    fn = ReprojectionError(torch.zeros(2, m, n, 2, device=device), torch.ones(2, m, n, device=device), m, n)
+    x0 = torch.zeros(2, p, device=device, requires_grad=True)
+    with pytest.raises(RuntimeError, match="no fused kernel"):
+        BFGSSolver(iterations=100, error_threshold=-1.0, minimum_step=-1.0).eval()(x0, fn)

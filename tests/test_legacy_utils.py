@@ -58,3 +58,30 @@ def test_secant_alpha_known_answers():
     assert out[3] == 0.5  # root 0.9999 is within 1e-3 of the upper end: midpoint
     assert out[4] == 0.5  # root 0.000999 within 1e-3 of the lower end: midpoint
     assert torch.isnan(out[5])  # NaN root kept (comparisons with NaN are false)
+
+
+def test_secant_alpha_gradient_is_finite_on_flat_rows():
+    """Equal slopes (rise == 0): the midpoint row passes 0.5 of the gradient to each bracket end
+    and 0 to the values, as the reference's InterpolateAlpha backward
+    (utils/func_interpolate_alpha.py:44-79) -- never 0 * inf = NaN from the unused secant branch."""
+    a1 = torch.tensor([0.0, 0.0], dtype=torch.float64, requires_grad=True)
+    a2 = torch.tensor([1.0, 1.0], dtype=torch.float64, requires_grad=True)
+    v1 = torch.tensor([2.0, -1.0], dtype=torch.float64, requires_grad=True)
+    v2 = torch.tensor([2.0, 3.0], dtype=torch.float64, requires_grad=True)
+    out = secant_alpha(a1, a2, v1, v2)
+    g = torch.autograd.grad(out.sum(), [a1, a2, v1, v2])
+    for t in g:
+        assert torch.isfinite(t).all()
+    assert g[0][0] == 0.5 and g[1][0] == 0.5 and g[2][0] == 0.0 and g[3][0] == 0.0
+    # secant row: root = a1 - v1 (a2 - a1) / (v2 - v1); d/da1 = v2 / rise, d/da2 = -v1 / rise,
+    # d/dv1 = -v2 (a2 - a1) / rise^2, d/dv2 = v1 (a2 - a1) / rise^2
+    assert torch.allclose(torch.stack([t[1] for t in g]),
+                          torch.tensor([3.0 / 4.0, 1.0 / 4.0, -3.0 / 16.0, -1.0 / 16.0], dtype=torch.float64))
+
+
+def test_secant_alpha_gradcheck():
+    a1 = torch.tensor([0.1, 0.9], dtype=torch.float64, requires_grad=True)
+    a2 = torch.tensor([0.8, 0.2], dtype=torch.float64, requires_grad=True)
+    v1 = torch.tensor([-1.3, 0.7], dtype=torch.float64, requires_grad=True)
+    v2 = torch.tensor([2.1, -0.4], dtype=torch.float64, requires_grad=True)
+    assert torch.autograd.gradcheck(secant_alpha, (a1, a2, v1, v2))

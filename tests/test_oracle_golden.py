@@ -250,3 +250,65 @@ def test_camera_l1_autograd_matches_reference(case, flags):
     for k, a in zip(camera_l1.PARAMETERS, got):
         want = g[f"{case}_{flags}_d_{k}"]
         assert np.allclose(a.numpy(), want, rtol=1e-10, atol=1e-12 * max(np.abs(want).max(), 1.0)), k
+
+
+# ---- Brown-Conrady, pinned to the reference's own distorted model (tests/golden/distortion.npz) ----
+
+@pytest.mark.parametrize("dt", ["f64", "f32"])
+def test_distorted_projection_matches_reference_bitwise(dt):
+    """distorted_camera_model.py:24-103 (_full_forward_model, loaded by path with the slot table
+    its test lists) on camera rows in the BA's tie (fx = fy = f, s = R = T = 0): u', v' and the
+    autograd gradients w.r.t. points and the BA parameters; the f64 case holds a z' == 0 point
+    (the model's nudge, :57).  Eager-mode reference bitwise; under TorchScript (the file's
+    decorator) the values are the same bits and the gradients within the executor's last-ulp
+    reordering."""
+    g = _load("distortion.npz")
+    key = f"proj_{dt}"
+    p = torch.tensor(g[key + "_points"]).requires_grad_(True)
+    x = torch.tensor(g[key + "_x"]).requires_grad_(True)
+    u, v = objective.distorted_rows(p, objective.camera_rows(x, 1))
+    loss = (u * torch.tensor(g[key + "_wu"])).sum() + (v * torch.tensor(g[key + "_wv"])).sum()
+    gp, gx = torch.autograd.grad(loss, [p, x])
+    assert np.array_equal(u.detach().numpy(), g[key + "_u"])
+    assert np.array_equal(v.detach().numpy(), g[key + "_v"])
+    assert np.array_equal(gp.numpy(), g[key + "_grad_points"])
+    assert np.array_equal(gx.numpy(), g[key + "_grad_x"])
+    assert np.array_equal(g[key + "_jit_u"], g[key + "_u"]) and np.array_equal(g[key + "_jit_v"], g[key + "_v"])
+    eps = np.finfo(g[key + "_u"].dtype).eps
+    for k, got in (("_grad_points", gp), ("_grad_x", gx)):
+        jit = g[key + "_jit" + k]
+        assert np.abs(got.numpy() - jit).max() <= 64 * eps * np.abs(jit).max(), k
+    if dt == "f64":
+        assert g[key + "_points"][2, 5, 2] == 0.0 and np.isfinite(g[key + "_u"][2, 5])
+
+
+@pytest.mark.parametrize("shape", list(SHAPES))
+@pytest.mark.parametrize("dt", ["f64", "f32"])
+def test_distorted_objective_and_gradient_match_reference_bitwise(shape, dt):
+    """The BA objective with the reference's distorted model (tests/golden/make_golden.py
+    ref_objective_bc): error and autograd gradient."""
+    g = _load("distortion.npz")
+    m, n = SHAPES[shape]
+    key = f"eval_{shape}_{dt}"
+    x = torch.tensor(g[key + "_x"]).requires_grad_(True)
+    e = objective.reprojection_error(x, torch.tensor(g[key + "_obs"]), torch.tensor(g[key + "_vis"]), m, n, True)
+    (grad,) = torch.autograd.grad(e.sum(), x)
+    assert np.array_equal(e.detach().numpy(), g[key + "_err"])
+    assert np.array_equal(grad.numpy(), g[key + "_grad"])
+    assert np.array_equal(g[key + "_jit_err"], g[key + "_err"])
+
+
+def test_distorted_trajectories_match_reference_bitwise():
+    """BFGSSolver().eval() on the headline model (C3 + Brown-Conrady, fp32) after K = 5, 20, 100:
+    the oracle reproduces the eager-mode reference bit for bit.  The reference's TorchScript mode
+    (same forward bits, its own symbolic backward) parts from it by ~1e-7 normwise at K = 100 and
+    by up to ~1e-3 on the five distortion coefficients -- the reference's own spread on that block."""
+    g = _load("distortion.npz")
+    x0 = torch.tensor(g["traj_c3_x0"])
+    fn = objective.ReprojectionClosure(torch.tensor(g["traj_c3_obs"]), torch.tensor(g["traj_c3_vis"]), 4, 256, True)
+    for k in (5, 20, 100):
+        out = solver.bfgs_solve(x0, fn, iterations=k, error_threshold=-1.0, minimum_step=-1.0)
+        assert np.array_equal(out.numpy(), g[f"traj_c3_k{k}"]), k
+        jit = torch.tensor(g[f"traj_c3_jit_k{k}"]).double()
+        rel = (jit - out.double()).norm(dim=-1) / out.double().norm(dim=-1)
+        assert rel.max() < 1e-6, (k, rel)
