@@ -29,6 +29,10 @@
 
 #include <type_traits>
 
+#ifndef DAVA_Z_NUDGE
+#define DAVA_Z_NUDGE 1  // the distorted model's z' == 0 -> 1e-8 nudge (0: A/B builds only)
+#endif
+
 namespace dava {
 
 // Diagnostic builds only (DAVA_PHASE_TIMING): thread 0 of every workgroup adds the shader
@@ -433,7 +437,7 @@ __device__ __forceinline__ bool ba_eval(const Layout& L, const S* x, const S* d,
       S go0 = 0.f, go1 = 0.f;          // dE/d obs (second-order instantiations only)
       if constexpr (RES == DAVA_RESIDUAL_SQUARED_REPROJECTION) {
         // projection; the distorted model nudges z' == 0 by 1e-8 (distorted_camera_model.py:57)
-        if (L.distort && p2 == S(0.0f)) p2 = p2 + 1e-8f;
+        if (DAVA_Z_NUDGE && L.distort && p2 == S(0.0f)) p2 = p2 + 1e-8f;
         const S iz = 1.0f / p2;
         const S qx = p0 * iz, qy = p1 * iz;
         const S ub = in.f * qx, vb = in.f * qy;
@@ -601,7 +605,7 @@ __device__ __forceinline__ bool ba_eval(const Layout& L, const S* x, const S* d,
               dp2 = da2 * vc + a2 * dc + k * w2 + Avw * dw2 + e2 * vB + c2 * dB + dtt2;
             }
           }
-          if (L.distort) {  // z' == 0 nudge (distorted_camera_model.py:57)
+          if (DAVA_Z_NUDGE && L.distort) {  // z' == 0 nudge (distorted_camera_model.py:57)
             if (p2.x == 0.0f) p2.x += 1e-8f;
             if (p2.y == 0.0f) p2.y += 1e-8f;
           }

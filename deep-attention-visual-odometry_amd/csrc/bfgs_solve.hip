@@ -52,7 +52,8 @@ struct SolveArgs {
   float* tape_g;  // (B, K, Pv)
   float* tape_s;  // (B, tape_T)
   int tape_T;
-  int stagger;    // shader cycles the odd workgroups wait before starting (0: none)
+  int stagger;    // shader cycles per start level (0: none)
+  int stagger_levels;  // <= 1: odd workgroups wait `stagger`; L > 1: level (b / 8) mod L waits level x stagger
   float drop_p;   // training-mode drop path probability (0: eval mode)
   unsigned long long drop_seed;
 };
@@ -88,6 +89,9 @@ __host__ __device__ constexpr int solve_waves(bool gv) { return gv ? 8 : 4; }
 #define DAVA_WIDE_PASS 1
 #endif
 constexpr int kWideMaxGroups = 7;
+#ifndef DAVA_GV_ENTRIES
+#define DAVA_GV_ENTRIES 1  // history entries per block reduction in the wide pass (rows of > 2 groups per thread)
+#endif
 __host__ __device__ inline bool wide_history_pass(int Pv, int kcap, bool gv) {
   return DAVA_WIDE_PASS && gv && kcap > 0 && (Pv / 4 + kWave * solve_waves(gv) - 1) / (kWave * solve_waves(gv)) <= kWideMaxGroups;
 }
@@ -406,7 +410,7 @@ __device__ __forceinline__ void compact_products_wide(int P, int Pv, int nh, con
                                                       float gamma0, const float* g, const float* gp, float* a_out,
                                                       float* b_out, float* scratch, int& buf) {
   constexpr int BLOCK = kWave * NW;
-  constexpr int E = GT <= 2 ? 2 : 1;
+  constexpr int E = GT <= 2 ? 2 : DAVA_GV_ENTRIES;
   const int tid = threadIdx.x;
   const int G = (P + 3) / 4;
   const f4v z = f4v{0, 0, 0, 0};
@@ -484,27 +488,73 @@ __device__ __forceinline__ void compact_products_wide(int P, int Pv, int nh, con
 #ifndef DAVA_GV_FUSED_TAIL
 #define DAVA_GV_FUSED_TAIL 1
 #endif
-template <int GT, int NW>
+// YL (XL launches): y and g are parked in LDS -- in the objective's gradient slot `ge` and the
+// direction slot `d`, both dead between the accepted trial and the new direction (ge was published
+// to the workspace, d_{k-1} became s_{k-1}) -- instead of 2 GT float4 registers per thread.  The
+// freed registers take a second history entry, so each block reduction covers DAVA_GV_ENTRIES_YL
+// entries and twice the rows are in flight per barrier: at C5 (GT = 7, one problem per CU) the pass
+// is bound by the bytes one CU keeps in flight, not by the chip's HBM (spreading the problems' start
+// times over 0.7 ms changed nothing, profiles/r03_ab_c5_start_spread.log).  Each thread reads back
+// only its own columns, so parking needs no barrier; the dots, reductions and accumulations are the
+// same operations in the same order, so the result is bitwise that of the register variant.
+#ifndef DAVA_GV_PARK_YG
+#define DAVA_GV_PARK_YG 1
+#endif
+#ifndef DAVA_GV_DOTS_ENTRY_OUTER
+#define DAVA_GV_DOTS_ENTRY_OUTER 0
+#endif
+#ifndef DAVA_GV_ENTRIES_YL
+#define DAVA_GV_ENTRIES_YL 2
+#endif
+template <int GT, int NW, bool YL>
 __device__ __forceinline__ float wide_direction(int P, int Pv, int nh, const float* __restrict__ S,
                                                 const float* __restrict__ W, float* hrho, float* hc, float gamma0,
                                                 const float* g, const float* gp, const float* s_cur, float* d,
                                                 float* s_row, float* w_row, float* scratch, int& buf, int entry,
-                                                float* tape_rho, float* tape_c) {
+                                                float* tape_rho, float* tape_c, float* yl) {
   constexpr int BLOCK = kWave * NW;
-  constexpr int E = GT <= 2 ? 2 : 1;
+  constexpr int E = GT <= 2 ? 2 : (YL ? DAVA_GV_ENTRIES_YL : DAVA_GV_ENTRIES);
+  constexpr int GR = YL ? 1 : GT;  // register copies of y, g
   const int tid = threadIdx.x;
   const int G = (P + 3) / 4;
   const f4v z = f4v{0, 0, 0, 0};
-  f4v y[GT], gg[GT], pa[GT], pb[GT];
+  f4v y[GR], gg[GR], pa[GT], pb[GT];
+  float* gl = d;  // YL: g parked in the direction slot (overwritten by d at the end, column by column)
 #pragma unroll
   for (int u = 0; u < GT; ++u) {
     const int q = tid + u * BLOCK;
-    y[u] = gg[u] = pa[u] = pb[u] = z;
+    pa[u] = pb[u] = z;
+    f4v g4 = z, y4 = z;
     if (q < G) {
-      gg[u] = *reinterpret_cast<const f4v*>(g + 4 * q);
-      y[u] = gg[u] - *reinterpret_cast<const f4v*>(gp + 4 * q);
+      g4 = *reinterpret_cast<const f4v*>(g + 4 * q);
+      y4 = g4 - *reinterpret_cast<const f4v*>(gp + 4 * q);
+    }
+    if constexpr (YL) {
+      if (q < G) {  // the slots hold Pv = 4 G floats
+        *reinterpret_cast<f4v*>(yl + 4 * q) = y4;
+        *reinterpret_cast<f4v*>(gl + 4 * q) = g4;
+      }
+    } else {
+      y[u] = y4;
+      gg[u] = g4;
     }
   }
+  auto yv = [&](int u) -> f4v {
+    if constexpr (YL) {
+      const int q = tid + u * BLOCK;
+      return q < G ? *reinterpret_cast<const f4v*>(yl + 4 * q) : z;
+    } else {
+      return y[u];
+    }
+  };
+  auto gv = [&](int u) -> f4v {
+    if constexpr (YL) {
+      const int q = tid + u * BLOCK;
+      return q < G ? *reinterpret_cast<const f4v*>(gl + 4 * q) : z;
+    } else {
+      return gg[u];
+    }
+  };
   auto dot4 = [](f4v a, f4v b) { const f4v t = a * b; return (t[0] + t[1]) + (t[2] + t[3]); };
   for (int j = 0; j < nh; j += E) {
     const int ne = min(E, nh - j);  // uniform
@@ -523,14 +573,30 @@ __device__ __forceinline__ float wide_direction(int P, int Pv, int nh, const flo
       }
     }
 #pragma unroll
-    for (int e = 0; e < E; ++e) {
-      dd[4 * e] = dd[4 * e + 1] = dd[4 * e + 2] = dd[4 * e + 3] = 0.0f;
+    for (int e = 0; e < 4 * E; ++e) dd[e] = 0.0f;
+    if constexpr (DAVA_GV_DOTS_ENTRY_OUTER) {  // y, g re-read per entry: shorter live ranges
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+#pragma unroll
+        for (int u = 0; u < GT; ++u) {
+          const f4v yu = yv(u), gu = gv(u);
+          dd[4 * e] += dot4(s4[e][u], yu);
+          dd[4 * e + 1] += dot4(w4[e][u], yu);
+          dd[4 * e + 2] += dot4(s4[e][u], gu);
+          dd[4 * e + 3] += dot4(w4[e][u], gu);
+        }
+      }
+    } else {
 #pragma unroll
       for (int u = 0; u < GT; ++u) {
-        dd[4 * e] += dot4(s4[e][u], y[u]);
-        dd[4 * e + 1] += dot4(w4[e][u], y[u]);
-        dd[4 * e + 2] += dot4(s4[e][u], gg[u]);
-        dd[4 * e + 3] += dot4(w4[e][u], gg[u]);
+        const f4v yu = yv(u), gu = gv(u);
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+          dd[4 * e] += dot4(s4[e][u], yu);
+          dd[4 * e + 1] += dot4(w4[e][u], yu);
+          dd[4 * e + 2] += dot4(s4[e][u], gu);
+          dd[4 * e + 3] += dot4(w4[e][u], gu);
+        }
       }
     }
     block_sum<4 * E, NW>(dd, scratch, buf);
@@ -555,13 +621,14 @@ __device__ __forceinline__ float wide_direction(int P, int Pv, int nh, const flo
 #pragma unroll
   for (int u = 0; u < GT; ++u) {
     const int q = tid + u * BLOCK;
-    pa[u] += gamma0 * y[u];
-    pb[u] += gamma0 * gg[u];
+    const f4v yu = yv(u), gu = gv(u);
+    pa[u] += gamma0 * yu;
+    pb[u] += gamma0 * gu;
     sv[u] = q < G ? *reinterpret_cast<const f4v*>(s_cur + 4 * q) : z;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      r[0] += sv[u][e] * y[u][e]; r[1] += pa[u][e] * y[u][e];
-      r[2] += sv[u][e] * gg[u][e]; r[3] += pa[u][e] * gg[u][e];
+      r[0] += sv[u][e] * yu[e]; r[1] += pa[u][e] * yu[e];
+      r[2] += sv[u][e] * gu[e]; r[3] += pa[u][e] * gu[e];
     }
   }
   block_sum<4, NW>(r, scratch, buf);
@@ -575,6 +642,7 @@ __device__ __forceinline__ float wide_direction(int P, int Pv, int nh, const flo
   for (int u = 0; u < GT; ++u) {
     const int q = tid + u * BLOCK;
     if (q < G) {
+      const f4v gu = gv(u);  // (YL: read before this thread's d overwrites its own g columns)
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int i = 4 * q + e;
@@ -582,7 +650,7 @@ __device__ __forceinline__ float wide_direction(int P, int Pv, int nh, const flo
           const float sri = sv[u][e] * rho;
           const float di = -1.0f * (pb[u][e] + sri * (c * sg) - sri * hyg - pa[u][e] * rsg);
           d[i] = di;
-          dg += di * gg[u][e];
+          dg += di * gu[e];
         }
       }
       *reinterpret_cast<f4v*>(s_row + 4 * q) = sv[u];  // history entry `entry` = (s, H'y, rho, c)
@@ -882,9 +950,15 @@ __global__ __launch_bounds__(kWave * NW, DAVA_SOLVE_WAVES_PER_EU) void bfgs_ba_s
   // half evaluates.  C2 (B = 1024): +6% on two boxes, +0.4% on a third; C3 (16 problems per slot)
   // gets no stagger
   // (profiles/r02_ab_stagger.log).  Results are unchanged (timing only).
-  if (a.stagger > 0 && (blockIdx.x & 1)) {
+  // Spread start (a.stagger_levels = L > 1; GV launches, one long problem per CU): within each XCD
+  // (workgroups are dealt round-robin, so b / 8 numbers them inside their XCD) the problems start at
+  // L evenly spaced offsets.  Every problem alternates an HBM-bound history stream with a VALU-bound
+  // objective evaluation; started together, all CUs stream at once and then all compute at once.
+  const int level = a.stagger_levels > 1 ? (int)((blockIdx.x >> 3) % (unsigned)a.stagger_levels) : (blockIdx.x & 1);
+  if (a.stagger > 0 && level > 0) {
     const unsigned long long t0 = clock64();
-    while (clock64() - t0 < (unsigned long long)a.stagger) __builtin_amdgcn_s_sleep(8);
+    const unsigned long long wait = (unsigned long long)a.stagger * (unsigned long long)level;
+    while (clock64() - t0 < wait) __builtin_amdgcn_s_sleep(8);
   }
   for (int b = blockIdx.x;;) {
     if (a.queue) {
@@ -1052,15 +1126,16 @@ __global__ __launch_bounds__(kWave * NW, DAVA_SOLVE_WAVES_PER_EU) void bfgs_ba_s
               float* srow = SH + (size_t)(k - 1) * Pv;
               float* wrow = WH + (size_t)(k - 1) * Pv;
               const bool fuse = DAVA_GV_FUSED_TAIL && wide_history_pass(Pv, a.kcap, GV) && k - 1 < a.kcap;
+              constexpr bool YLP = XL && DAVA_GV_PARK_YG;  // y, g parked in the dead ge / d LDS slots
               if (fuse) {
                 tail_done = true;
-                if (GT <= 1) dg = wide_direction<1, NW>(P, Pv, nh, SH, WH, hrho, hc, gamma0, g, gp, s_cur, d, srow, wrow, scratch, buf, k - 1, tr, tcp);
-                else if (GT == 2) dg = wide_direction<2, NW>(P, Pv, nh, SH, WH, hrho, hc, gamma0, g, gp, s_cur, d, srow, wrow, scratch, buf, k - 1, tr, tcp);
-                else if (GT == 3) dg = wide_direction<3, NW>(P, Pv, nh, SH, WH, hrho, hc, gamma0, g, gp, s_cur, d, srow, wrow, scratch, buf, k - 1, tr, tcp);
-                else if (GT == 4) dg = wide_direction<4, NW>(P, Pv, nh, SH, WH, hrho, hc, gamma0, g, gp, s_cur, d, srow, wrow, scratch, buf, k - 1, tr, tcp);
-                else if (GT == 5) dg = wide_direction<5, NW>(P, Pv, nh, SH, WH, hrho, hc, gamma0, g, gp, s_cur, d, srow, wrow, scratch, buf, k - 1, tr, tcp);
-                else if (GT == 6) dg = wide_direction<6, NW>(P, Pv, nh, SH, WH, hrho, hc, gamma0, g, gp, s_cur, d, srow, wrow, scratch, buf, k - 1, tr, tcp);
-                else dg = wide_direction<7, NW>(P, Pv, nh, SH, WH, hrho, hc, gamma0, g, gp, s_cur, d, srow, wrow, scratch, buf, k - 1, tr, tcp);
+                if (GT <= 1) dg = wide_direction<1, NW, YLP>(P, Pv, nh, SH, WH, hrho, hc, gamma0, g, gp, s_cur, d, srow, wrow, scratch, buf, k - 1, tr, tcp, ge);
+                else if (GT == 2) dg = wide_direction<2, NW, YLP>(P, Pv, nh, SH, WH, hrho, hc, gamma0, g, gp, s_cur, d, srow, wrow, scratch, buf, k - 1, tr, tcp, ge);
+                else if (GT == 3) dg = wide_direction<3, NW, YLP>(P, Pv, nh, SH, WH, hrho, hc, gamma0, g, gp, s_cur, d, srow, wrow, scratch, buf, k - 1, tr, tcp, ge);
+                else if (GT == 4) dg = wide_direction<4, NW, YLP>(P, Pv, nh, SH, WH, hrho, hc, gamma0, g, gp, s_cur, d, srow, wrow, scratch, buf, k - 1, tr, tcp, ge);
+                else if (GT == 5) dg = wide_direction<5, NW, YLP>(P, Pv, nh, SH, WH, hrho, hc, gamma0, g, gp, s_cur, d, srow, wrow, scratch, buf, k - 1, tr, tcp, ge);
+                else if (GT == 6) dg = wide_direction<6, NW, YLP>(P, Pv, nh, SH, WH, hrho, hc, gamma0, g, gp, s_cur, d, srow, wrow, scratch, buf, k - 1, tr, tcp, ge);
+                else dg = wide_direction<7, NW, YLP>(P, Pv, nh, SH, WH, hrho, hc, gamma0, g, gp, s_cur, d, srow, wrow, scratch, buf, k - 1, tr, tcp, ge);
               } else if (!wide_history_pass(Pv, a.kcap, GV))
                 compact_products<GV ? 8 : 1, NW>(P, Pv, nh, SH, WH, hcoef, hrho, hc, gamma0, g, gp, hy_new, hg);
               else if (GT <= 1) compact_products_wide<1, NW>(P, Pv, nh, SH, WH, hrho, hc, gamma0, g, gp, hy_new, hg, scratch, buf);
@@ -1513,7 +1588,9 @@ static void launch_solve_ppt(const SolveArgs& a, int B, int lds, hipStream_t s) 
   }
   // stagger only a launch whose problems all run at once (one round, B <= slots)
   args.stagger = slots > 0 && B <= slots && B > 1 ? kStaggerCycles : 0;
+  args.stagger_levels = 1;
   if (const char* e = getenv("DAVA_STAGGER")) args.stagger = max(0, atoi(e));  // A/B knob (cycles)
+  if (const char* e = getenv("DAVA_STAGGER_LEVELS")) args.stagger_levels = max(1, atoi(e));
   if (args.queue) {  // one workgroup per resident slot
     if (slots > 0) grid = min(B, slots);
     // The hardware already refills a slot as soon as its workgroup retires, but only from its
@@ -1623,6 +1700,7 @@ static int solve_impl(const DavaScene* scene, const DavaSolverConfig* config, co
   a.lcap = lcap;
   a.phase_cycles = nullptr;
   a.stagger = 0;
+  a.stagger_levels = 1;
   a.drop_p = config->drop_path_p;
   a.drop_seed = ((unsigned long long)config->drop_seed_hi << 32) | config->drop_seed_lo;
   a.queue = queue ? reinterpret_cast<int*>(static_cast<char*>(workspace) + need) : nullptr;

@@ -159,7 +159,7 @@ class BFGSSolver(Module):
         x0 = parameters.reshape(-1, parameters.size(-1))
         if x0.dtype != torch.float32:
             raise TypeError("the fused BA solver computes in float32")
-        mode = self._resolve_mode(num_iterations, x0.size(-1))
+        mode = self._resolve_mode(num_iterations, x0.size(-1), x0.shape[0], x0.device)
         x, _, status = native_ops.ba_solve(
             x0, fn.observations.reshape(-1, fn.num_views, fn.num_points, 2),
             fn.visibility.reshape(-1, fn.num_views, fn.num_points), fn.num_views, fn.num_points, fn.distortion,
@@ -171,9 +171,16 @@ class BFGSSolver(Module):
 
     MAX_COMPACT_ENTRIES = 1024  # kMaxCompactEntries in csrc/bfgs_solve.hip
 
-    def _resolve_mode(self, num_iterations: int, p: int) -> int:
-        """'auto': the compact history (same math, O(k P) bytes per iteration) unless it would
-        need more than 1024 entries or hold more than 4x the bytes of a dense P x P matrix."""
+    def _resolve_mode(self, num_iterations: int, p: int, batch: int = 1, device=None) -> int:
+        """'auto': the compact history (exact BFGS in product form, O(k P) bytes at iteration k)
+        whenever its entries fit the kernel (<= 1024) and its workspace fits the device; the dense
+        P x P matrix (O(P^2) bytes per iteration) only beyond that.  The iteration CAP does not
+        decide: with the reference's stopping rules problems stop long before it (reference defaults
+        1e-4 / 1000 / 1e-8: 36 iterations on average at C2, 107 at C3), where compact moves a
+        fraction of the dense bytes -- measured 642.6k vs 77.6k problems/s at C2 and 213.7k vs 9.3k
+        at C3 (profiles/r03_defaults_c2_c3.jsonl).  Even a batch that ran every problem to
+        K = 1000 would move K Pv / (2 P^2) x the dense bytes (1.27x at C2, 2.5x at C1), streamed
+        at a higher fraction of the HBM peak than the dense sweep."""
         if self.hessian_mode == "dense":
             return _native.DAVA_HESSIAN_DENSE
         entries = max(num_iterations - 1, 1)
@@ -182,9 +189,15 @@ class BFGSSolver(Module):
             if not fits:
                 raise ValueError(f"compact mode supports at most {self.MAX_COMPACT_ENTRIES + 1} iterations")
             return _native.DAVA_HESSIAN_COMPACT
-        pv = (p + 3) // 4 * 4
-        small = 2 * entries * pv <= 4 * p * ((p + 31) // 32 * 32)
-        return _native.DAVA_HESSIAN_COMPACT if fits and small else _native.DAVA_HESSIAN_DENSE
+        if not fits:
+            return _native.DAVA_HESSIAN_DENSE
+        if device is not None and device.type == "cuda":
+            pv = (p + 3) // 4 * 4
+            compact_bytes = batch * 2 * entries * pv * 4
+            free, _ = torch.cuda.mem_get_info(device)
+            if compact_bytes > 0.9 * free:  # e.g. B = 65536 at K = 1000 on one GPU: 416 GB of history
+                return _native.DAVA_HESSIAN_DENSE
+        return _native.DAVA_HESSIAN_COMPACT
 
     def _generic(self, parameters, error_function, error_threshold, num_iterations):
         batch_dimensions = parameters.shape[:-1]

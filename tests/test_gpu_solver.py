@@ -99,31 +99,24 @@ def _report(tag, rel, env=None, extra=None):
 def _check_k100(out, ref, x0, obs, vis, m, n, distortion, env, env_intrinsics=None, tag=None):
     """Parity after K = 100 iterations, where small two-view problems run into fp32 stagnation.
 
-    Two builds of this kernel that differ only in FMA contraction (register- vs LDS-resident
-    points in the objective) agree with each other and with the reference to <= 2e-8 at K = 20,
-    yet at K = 100 each puts a different single problem 1.6e-5 .. 4.2e-5 away -- a line-search
-    comparison that is a near tie takes the other branch (tools/dump_solve.py,
-    profiles/r01_parity_spread.log).  The reference itself does the same across host CPUs (a
-    C1 problem moves 4.1e-5 under a 1-ulp nudge of x0 on one CPU and not on another).  So every
-    problem is held to max(1e-5, 10x the reference's own 1-ulp sensitivity) OR, as SURVEY.md 0.6
-    prescribes for runs to stagnation, to the objective value (within 5% of the reference's,
-    or five orders of magnitude below the start), and most problems must still agree to 1e-5.
-    """
+    Every problem must lie within max(1e-5, 10x the reference's own 1-ulp sensitivity) -- the
+    envelope -- and within 1e-5 outright.  (Round 1 allowed one problem per case to fall back to an
+    objective-value comparison, because two builds that differed only in FMA contraction each put a
+    different single C1/C2 problem 1.6e-5 .. 4.2e-5 away at K = 100 -- a near-tie line-search branch
+    at fp32 stagnation (tools/dump_solve.py, profiles/r01_parity_spread.log).  Since round 2 every
+    distribution has all problems <= 1e-5 with no fallback used (profiles/r03*_parity_distribution.jsonl),
+    so the bar is the strict one.)  The objective reached is still reported."""
     rel = _rel(out, ref)
     e_gpu = objective.reprojection_error(out.double(), obs.double(), vis, m, n, distortion)
     e_ref = objective.reprojection_error(ref.double(), obs.double(), vis, m, n, distortion)
-    e_0 = objective.reprojection_error(x0.double(), obs.double(), vis, m, n, distortion)
-    same_objective = e_gpu <= torch.maximum(e_ref * 1.05, 1e-5 * e_0)
     outside = rel > env
     if tag is not None:
-        _report(tag, rel, env, {"n_objective_fallback": int(outside.sum())})
-    # every problem within its envelope, or (a near-tie branch at fp32 stagnation) at the same objective
-    assert (~outside | same_objective).all(), (rel.tolist(), env.tolist(), e_gpu.tolist(), e_ref.tolist())
-    # ... and the objective fallback is the exception: at most one problem per case
-    assert int(outside.sum()) <= 1, (rel.tolist(), env.tolist())
+        _report(tag, rel, env, {"n_objective_fallback": 0,
+                                "max_objective_ratio": float((e_gpu / e_ref.clamp(min=1e-30)).max())})
+    assert not outside.any(), (rel.tolist(), env.tolist(), e_gpu.tolist(), e_ref.tolist())
+    assert (rel <= TOL).all(), rel
     if env_intrinsics is not None:
-        assert ((_rel(out[:, :3], ref[:, :3]) <= env_intrinsics) | same_objective).all()
-    assert (rel <= TOL).double().mean() >= 0.9, rel
+        assert (_rel(out[:, :3], ref[:, :3]) <= env_intrinsics).all()
 
 
 @pytest.mark.parametrize("mode", ["dense", "compact"])
@@ -237,10 +230,6 @@ def test_reference_golden_distorted_trajectories(device, mode):
         rel, rel_d = _rel(out, ref), _rel(out[:, -5:], ref[:, -5:])
         jit_d = _rel(torch.tensor(g[f"traj_c3_jit_k{k}"])[:, -5:], ref[:, -5:])
         assert (status[:, 0] == k).all()
-        if k <= 20:
-            _report(f"golden_bc_{mode}_c3_K{k}", rel, None, {"distortion_max_rel": float(rel_d.max())})
-            assert rel.max() <= TOL, (k, rel)
-            continue
         kw = dict(iterations=k, error_threshold=-1.0, minimum_step=-1.0)
         env, env_i, env_d = _envelopes(x0, fn, ref, distortion=True, **kw)
         _report(f"golden_bc_{mode}_c3_K{k}", rel, env,
@@ -660,3 +649,28 @@ def test_infeasible_generic_fallback_raises(device):
     x0 = torch.zeros(2, p, device=device, requires_grad=True)
     with pytest.raises(RuntimeError, match="no fused kernel"):
         BFGSSolver(iterations=100, error_threshold=-1.0, minimum_step=-1.0).eval()(x0, fn)
+
+
+def test_reference_defaults_c2_objective_parity(device):
+    """BFGSSolver() with the reference's DEFAULT kwargs (error 1e-4, 1000 iterations, min step 1e-8)
+    through the module on C2-shaped problems (runs to the stopping rules are judged by
+    the objective reached).  The module picks the compact history (the cap no longer forces the
+    dense matrix), every problem stops by a rule, and each reaches the oracle's objective (within
+    5%, or below the error threshold as the reference stops there)."""
+    from deep_attention_visual_odometry_amd import BFGSSolver, _native
+
+    x0, obs, vis = _scene(16, 2, 128, False, 901)
+    s = BFGSSolver().eval()
+    assert s._resolve_mode(s.iterations, x0.shape[1], 16, device) == _native.DAVA_HESSIAN_COMPACT
+    out, status = _gpu_solve(device, x0, obs, vis, 2, 128, False)
+    fn = objective.ReprojectionClosure(obs, vis, 2, 128)
+    rec = solver.SolveRecord(None, None)
+    ref = solver.bfgs_solve(x0, fn, record=rec)
+    e_gpu = objective.reprojection_error(out.double(), obs.double(), vis, 2, 128)
+    e_ref = objective.reprojection_error(ref.double(), obs.double(), vis, 2, 128)
+    _report("defaults_C2_B16", _rel(out, ref), None,
+            {"e_gpu_max": float(e_gpu.max()), "e_ref_max": float(e_ref.max()),
+             "steps_gpu_mean": float(status[:, 0].double().mean()),
+             "steps_ref_mean": float(rec.iterations.double().mean())})
+    assert (status[:, 1] != 0).all()  # stopped by a rule, not the cap
+    assert (e_gpu <= 1.05 * torch.clamp(e_ref, min=1e-4)).all(), (e_gpu, e_ref)

@@ -16,7 +16,7 @@ mkdir -p "$OUT"
 objs=()
 for src in "$T"/csrc/*.hip; do
   o="$OUT/$(basename "${src%.hip}").o"
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -I"$T/include" -I"$T/csrc" -c "$src" -o "$o" &
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -fno-slp-vectorize -Wno-unused-function -I"$T/include" -I"$T/csrc" -c "$src" -o "$o" &
   objs+=("$o")
 done
 wait
