@@ -37,6 +37,17 @@ from ..camera_model import ReprojectionError
 from .line_search import line_search_wolfe_conditions
 
 
+def _free_device_bytes(device) -> float:
+    """Free memory on `device` (inf when it cannot be asked: tracing under torch.compile or fake
+    tensors, where the choice must not touch the device)."""
+    if device is None or device.type != "cuda" or torch.compiler.is_compiling():
+        return float("inf")
+    try:
+        return float(torch.cuda.mem_get_info(device)[0])
+    except RuntimeError:
+        return float("inf")
+
+
 class BFGSSolver(Module):
     """Broyden-Fletcher-Goldfarb-Shanno with a dense inverse Hessian per problem and a
     strong-Wolfe line search (Nocedal & Wright 2009, eq. 6.17, 6.20; alg. 3.5/3.6)."""
@@ -116,7 +127,7 @@ class BFGSSolver(Module):
         p = parameters.size(-1)
         per_matrix = b * p * p * parameters.element_size()
         need = per_matrix * (3 * num_iterations + 2 if parameters.requires_grad else 8)
-        free, _ = torch.cuda.mem_get_info(parameters.device)
+        free = _free_device_bytes(parameters.device)
         if need > free:
             what = ("differentiating through the solve" if parameters.requires_grad
                     else "training mode with return_second_last")
@@ -191,12 +202,10 @@ class BFGSSolver(Module):
             return _native.DAVA_HESSIAN_COMPACT
         if not fits:
             return _native.DAVA_HESSIAN_DENSE
-        if device is not None and device.type == "cuda":
-            pv = (p + 3) // 4 * 4
-            compact_bytes = batch * 2 * entries * pv * 4
-            free, _ = torch.cuda.mem_get_info(device)
-            if compact_bytes > 0.9 * free:  # e.g. B = 65536 at K = 1000 on one GPU: 416 GB of history
-                return _native.DAVA_HESSIAN_DENSE
+        pv = (p + 3) // 4 * 4
+        compact_bytes = batch * 2 * entries * pv * 4
+        if compact_bytes > 0.9 * _free_device_bytes(device):  # e.g. B = 65536, K = 1000: 416 GB of history
+            return _native.DAVA_HESSIAN_DENSE
         return _native.DAVA_HESSIAN_COMPACT
 
     def _generic(self, parameters, error_function, error_threshold, num_iterations):
