@@ -488,73 +488,33 @@ __device__ __forceinline__ void compact_products_wide(int P, int Pv, int nh, con
 #ifndef DAVA_GV_FUSED_TAIL
 #define DAVA_GV_FUSED_TAIL 1
 #endif
-// YL (XL launches): y and g are parked in LDS -- in the objective's gradient slot `ge` and the
-// direction slot `d`, both dead between the accepted trial and the new direction (ge was published
-// to the workspace, d_{k-1} became s_{k-1}) -- instead of 2 GT float4 registers per thread.  The
-// freed registers take a second history entry, so each block reduction covers DAVA_GV_ENTRIES_YL
-// entries and twice the rows are in flight per barrier: at C5 (GT = 7, one problem per CU) the pass
-// is bound by the bytes one CU keeps in flight, not by the chip's HBM (spreading the problems' start
-// times over 0.7 ms changed nothing, profiles/r03_ab_c5_start_spread.log).  Each thread reads back
-// only its own columns, so parking needs no barrier; the dots, reductions and accumulations are the
-// same operations in the same order, so the result is bitwise that of the register variant.
-#ifndef DAVA_GV_PARK_YG
-#define DAVA_GV_PARK_YG 1
-#endif
-#ifndef DAVA_GV_DOTS_ENTRY_OUTER
-#define DAVA_GV_DOTS_ENTRY_OUTER 0
-#endif
-#ifndef DAVA_GV_ENTRIES_YL
-#define DAVA_GV_ENTRIES_YL 2
-#endif
-template <int GT, int NW, bool YL>
+// Per entry the four dots are packed 2-wide FMA chains over this thread's groups (v_pk_fma_f32,
+// as the LDS-mode pass does, DAVA_PACKED_HISTORY) and the contributions to H'y, H'g packed FMAs:
+// at C5 (GT = 7) ~250 VALU ops per entry and wave instead of ~420.  (Rejected, interleaved A/B,
+// profiles/r03_ab_c5_park_yg_lds.log: parking y and g in the dead LDS gradient / direction slots to
+// free registers for two entries per reduction -- bitwise equal, but the per-entry LDS re-reads and
+// the spills cost 14% with one entry and 19% with two.)
+template <int GT, int NW>
 __device__ __forceinline__ float wide_direction(int P, int Pv, int nh, const float* __restrict__ S,
                                                 const float* __restrict__ W, float* hrho, float* hc, float gamma0,
                                                 const float* g, const float* gp, const float* s_cur, float* d,
                                                 float* s_row, float* w_row, float* scratch, int& buf, int entry,
-                                                float* tape_rho, float* tape_c, float* yl) {
+                                                float* tape_rho, float* tape_c) {
   constexpr int BLOCK = kWave * NW;
-  constexpr int E = GT <= 2 ? 2 : (YL ? DAVA_GV_ENTRIES_YL : DAVA_GV_ENTRIES);
-  constexpr int GR = YL ? 1 : GT;  // register copies of y, g
+  constexpr int E = GT <= 2 ? 2 : DAVA_GV_ENTRIES;
   const int tid = threadIdx.x;
   const int G = (P + 3) / 4;
   const f4v z = f4v{0, 0, 0, 0};
-  f4v y[GR], gg[GR], pa[GT], pb[GT];
-  float* gl = d;  // YL: g parked in the direction slot (overwritten by d at the end, column by column)
+  f4v y[GT], gg[GT], pa[GT], pb[GT];
 #pragma unroll
   for (int u = 0; u < GT; ++u) {
     const int q = tid + u * BLOCK;
-    pa[u] = pb[u] = z;
-    f4v g4 = z, y4 = z;
+    y[u] = gg[u] = pa[u] = pb[u] = z;
     if (q < G) {
-      g4 = *reinterpret_cast<const f4v*>(g + 4 * q);
-      y4 = g4 - *reinterpret_cast<const f4v*>(gp + 4 * q);
-    }
-    if constexpr (YL) {
-      if (q < G) {  // the slots hold Pv = 4 G floats
-        *reinterpret_cast<f4v*>(yl + 4 * q) = y4;
-        *reinterpret_cast<f4v*>(gl + 4 * q) = g4;
-      }
-    } else {
-      y[u] = y4;
-      gg[u] = g4;
+      gg[u] = *reinterpret_cast<const f4v*>(g + 4 * q);
+      y[u] = gg[u] - *reinterpret_cast<const f4v*>(gp + 4 * q);
     }
   }
-  auto yv = [&](int u) -> f4v {
-    if constexpr (YL) {
-      const int q = tid + u * BLOCK;
-      return q < G ? *reinterpret_cast<const f4v*>(yl + 4 * q) : z;
-    } else {
-      return y[u];
-    }
-  };
-  auto gv = [&](int u) -> f4v {
-    if constexpr (YL) {
-      const int q = tid + u * BLOCK;
-      return q < G ? *reinterpret_cast<const f4v*>(gl + 4 * q) : z;
-    } else {
-      return gg[u];
-    }
-  };
   auto dot4 = [](f4v a, f4v b) { const f4v t = a * b; return (t[0] + t[1]) + (t[2] + t[3]); };
   for (int j = 0; j < nh; j += E) {
     const int ne = min(E, nh - j);  // uniform
@@ -573,31 +533,30 @@ __device__ __forceinline__ float wide_direction(int P, int Pv, int nh, const flo
       }
     }
 #pragma unroll
-    for (int e = 0; e < 4 * E; ++e) dd[e] = 0.0f;
-    if constexpr (DAVA_GV_DOTS_ENTRY_OUTER) {  // y, g re-read per entry: shorter live ranges
-#pragma unroll
-      for (int e = 0; e < E; ++e) {
-#pragma unroll
-        for (int u = 0; u < GT; ++u) {
-          const f4v yu = yv(u), gu = gv(u);
-          dd[4 * e] += dot4(s4[e][u], yu);
-          dd[4 * e + 1] += dot4(w4[e][u], yu);
-          dd[4 * e + 2] += dot4(s4[e][u], gu);
-          dd[4 * e + 3] += dot4(w4[e][u], gu);
-        }
-      }
-    } else {
+    for (int e = 0; e < E; ++e) {
+#if DAVA_PACKED_HISTORY
+      f2v sy2 = {0.f, 0.f}, wy2 = {0.f, 0.f}, sg2 = {0.f, 0.f}, wg2 = {0.f, 0.f};
 #pragma unroll
       for (int u = 0; u < GT; ++u) {
-        const f4v yu = yv(u), gu = gv(u);
-#pragma unroll
-        for (int e = 0; e < E; ++e) {
-          dd[4 * e] += dot4(s4[e][u], yu);
-          dd[4 * e + 1] += dot4(w4[e][u], yu);
-          dd[4 * e + 2] += dot4(s4[e][u], gu);
-          dd[4 * e + 3] += dot4(w4[e][u], gu);
-        }
+        sy2 = pk_fma(s4[e][u].lo, y[u].lo, sy2); sy2 = pk_fma(s4[e][u].hi, y[u].hi, sy2);
+        wy2 = pk_fma(w4[e][u].lo, y[u].lo, wy2); wy2 = pk_fma(w4[e][u].hi, y[u].hi, wy2);
+        sg2 = pk_fma(s4[e][u].lo, gg[u].lo, sg2); sg2 = pk_fma(s4[e][u].hi, gg[u].hi, sg2);
+        wg2 = pk_fma(w4[e][u].lo, gg[u].lo, wg2); wg2 = pk_fma(w4[e][u].hi, gg[u].hi, wg2);
       }
+      dd[4 * e] = sy2.x + sy2.y;
+      dd[4 * e + 1] = wy2.x + wy2.y;
+      dd[4 * e + 2] = sg2.x + sg2.y;
+      dd[4 * e + 3] = wg2.x + wg2.y;
+#else
+      dd[4 * e] = dd[4 * e + 1] = dd[4 * e + 2] = dd[4 * e + 3] = 0.0f;
+#pragma unroll
+      for (int u = 0; u < GT; ++u) {
+        dd[4 * e] += dot4(s4[e][u], y[u]);
+        dd[4 * e + 1] += dot4(w4[e][u], y[u]);
+        dd[4 * e + 2] += dot4(s4[e][u], gg[u]);
+        dd[4 * e + 3] += dot4(w4[e][u], gg[u]);
+      }
+#endif
     }
     block_sum<4 * E, NW>(dd, scratch, buf);
     buf ^= 1;
@@ -605,6 +564,15 @@ __device__ __forceinline__ float wide_direction(int P, int Pv, int nh, const flo
     for (int e = 0; e < E; ++e) {
       if (e < ne) {
         const float rho = hrho[j + e], cr = hc[j + e] * rho;
+#if DAVA_PACKED_HISTORY
+        const float ay = fmaf(cr, dd[4 * e], -(rho * dd[4 * e + 1])), by = -rho * dd[4 * e];
+        const float ag = fmaf(cr, dd[4 * e + 2], -(rho * dd[4 * e + 3])), bg = -rho * dd[4 * e + 2];
+#pragma unroll
+        for (int u = 0; u < GT; ++u) {
+          pa[u] = pk_fma4(by, w4[e][u], pk_fma4(ay, s4[e][u], pa[u]));
+          pb[u] = pk_fma4(bg, w4[e][u], pk_fma4(ag, s4[e][u], pb[u]));
+        }
+#else
         const float ay = cr * dd[4 * e] - rho * dd[4 * e + 1], by = -rho * dd[4 * e];
         const float ag = cr * dd[4 * e + 2] - rho * dd[4 * e + 3], bg = -rho * dd[4 * e + 2];
 #pragma unroll
@@ -612,6 +580,7 @@ __device__ __forceinline__ float wide_direction(int P, int Pv, int nh, const flo
           pa[u] += ay * s4[e][u] + by * w4[e][u];
           pb[u] += ag * s4[e][u] + bg * w4[e][u];
         }
+#endif
       }
     }
   }
@@ -621,7 +590,7 @@ __device__ __forceinline__ float wide_direction(int P, int Pv, int nh, const flo
 #pragma unroll
   for (int u = 0; u < GT; ++u) {
     const int q = tid + u * BLOCK;
-    const f4v yu = yv(u), gu = gv(u);
+    const f4v yu = y[u], gu = gg[u];
     pa[u] += gamma0 * yu;
     pb[u] += gamma0 * gu;
     sv[u] = q < G ? *reinterpret_cast<const f4v*>(s_cur + 4 * q) : z;
@@ -642,7 +611,7 @@ __device__ __forceinline__ float wide_direction(int P, int Pv, int nh, const flo
   for (int u = 0; u < GT; ++u) {
     const int q = tid + u * BLOCK;
     if (q < G) {
-      const f4v gu = gv(u);  // (YL: read before this thread's d overwrites its own g columns)
+      const f4v gu = gg[u];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int i = 4 * q + e;
@@ -1126,16 +1095,15 @@ __global__ __launch_bounds__(kWave * NW, DAVA_SOLVE_WAVES_PER_EU) void bfgs_ba_s
               float* srow = SH + (size_t)(k - 1) * Pv;
               float* wrow = WH + (size_t)(k - 1) * Pv;
               const bool fuse = DAVA_GV_FUSED_TAIL && wide_history_pass(Pv, a.kcap, GV) && k - 1 < a.kcap;
-              constexpr bool YLP = XL && DAVA_GV_PARK_YG;  // y, g parked in the dead ge / d LDS slots
               if (fuse) {
                 tail_done = true;
-                if (GT <= 1) dg = wide_direction<1, NW, YLP>(P, Pv, nh, SH, WH, hrho, hc, gamma0, g, gp, s_cur, d, srow, wrow, scratch, buf, k - 1, tr, tcp, ge);
-                else if (GT == 2) dg = wide_direction<2, NW, YLP>(P, Pv, nh, SH, WH, hrho, hc, gamma0, g, gp, s_cur, d, srow, wrow, scratch, buf, k - 1, tr, tcp, ge);
-                else if (GT == 3) dg = wide_direction<3, NW, YLP>(P, Pv, nh, SH, WH, hrho, hc, gamma0, g, gp, s_cur, d, srow, wrow, scratch, buf, k - 1, tr, tcp, ge);
-                else if (GT == 4) dg = wide_direction<4, NW, YLP>(P, Pv, nh, SH, WH, hrho, hc, gamma0, g, gp, s_cur, d, srow, wrow, scratch, buf, k - 1, tr, tcp, ge);
-                else if (GT == 5) dg = wide_direction<5, NW, YLP>(P, Pv, nh, SH, WH, hrho, hc, gamma0, g, gp, s_cur, d, srow, wrow, scratch, buf, k - 1, tr, tcp, ge);
-                else if (GT == 6) dg = wide_direction<6, NW, YLP>(P, Pv, nh, SH, WH, hrho, hc, gamma0, g, gp, s_cur, d, srow, wrow, scratch, buf, k - 1, tr, tcp, ge);
-                else dg = wide_direction<7, NW, YLP>(P, Pv, nh, SH, WH, hrho, hc, gamma0, g, gp, s_cur, d, srow, wrow, scratch, buf, k - 1, tr, tcp, ge);
+                if (GT <= 1) dg = wide_direction<1, NW>(P, Pv, nh, SH, WH, hrho, hc, gamma0, g, gp, s_cur, d, srow, wrow, scratch, buf, k - 1, tr, tcp);
+                else if (GT == 2) dg = wide_direction<2, NW>(P, Pv, nh, SH, WH, hrho, hc, gamma0, g, gp, s_cur, d, srow, wrow, scratch, buf, k - 1, tr, tcp);
+                else if (GT == 3) dg = wide_direction<3, NW>(P, Pv, nh, SH, WH, hrho, hc, gamma0, g, gp, s_cur, d, srow, wrow, scratch, buf, k - 1, tr, tcp);
+                else if (GT == 4) dg = wide_direction<4, NW>(P, Pv, nh, SH, WH, hrho, hc, gamma0, g, gp, s_cur, d, srow, wrow, scratch, buf, k - 1, tr, tcp);
+                else if (GT == 5) dg = wide_direction<5, NW>(P, Pv, nh, SH, WH, hrho, hc, gamma0, g, gp, s_cur, d, srow, wrow, scratch, buf, k - 1, tr, tcp);
+                else if (GT == 6) dg = wide_direction<6, NW>(P, Pv, nh, SH, WH, hrho, hc, gamma0, g, gp, s_cur, d, srow, wrow, scratch, buf, k - 1, tr, tcp);
+                else dg = wide_direction<7, NW>(P, Pv, nh, SH, WH, hrho, hc, gamma0, g, gp, s_cur, d, srow, wrow, scratch, buf, k - 1, tr, tcp);
               } else if (!wide_history_pass(Pv, a.kcap, GV))
                 compact_products<GV ? 8 : 1, NW>(P, Pv, nh, SH, WH, hcoef, hrho, hc, gamma0, g, gp, hy_new, hg);
               else if (GT <= 1) compact_products_wide<1, NW>(P, Pv, nh, SH, WH, hrho, hc, gamma0, g, gp, hy_new, hg, scratch, buf);
