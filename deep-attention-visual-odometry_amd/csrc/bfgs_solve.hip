@@ -515,7 +515,6 @@ __device__ __forceinline__ float wide_direction(int P, int Pv, int nh, const flo
       y[u] = gg[u] - *reinterpret_cast<const f4v*>(gp + 4 * q);
     }
   }
-  auto dot4 = [](f4v a, f4v b) { const f4v t = a * b; return (t[0] + t[1]) + (t[2] + t[3]); };
   for (int j = 0; j < nh; j += E) {
     const int ne = min(E, nh - j);  // uniform
     f4v s4[E][GT], w4[E][GT];
@@ -548,6 +547,7 @@ __device__ __forceinline__ float wide_direction(int P, int Pv, int nh, const flo
       dd[4 * e + 2] = sg2.x + sg2.y;
       dd[4 * e + 3] = wg2.x + wg2.y;
 #else
+      auto dot4 = [](f4v a, f4v b) { const f4v t = a * b; return (t[0] + t[1]) + (t[2] + t[3]); };
       dd[4 * e] = dd[4 * e + 1] = dd[4 * e + 2] = dd[4 * e + 3] = 0.0f;
 #pragma unroll
       for (int u = 0; u < GT; ++u) {
@@ -671,6 +671,10 @@ __device__ __forceinline__ float wide_direction(int P, int Pv, int nh, const flo
 #ifndef DAVA_FUSED_INFLIGHT_LARGE
 #define DAVA_FUSED_INFLIGHT_LARGE 2  // 3-4 groups per lane (P <= 1024; C3)
 #endif
+// LDS-DMA staging (rejected, r03): EF register entries plus 1-3 more per wave copied HBM -> LDS by
+// global_load_lds_dwordx4 (no VGPRs) in the same batch, in the LDS the resident entries use --
+// bitwise equal, but C2 -2..-5% and C1 (B = 8192) -3..-5%: the resident entries are worth more
+// than the deeper batch (profiles/r03_ab_c2_lds_dma_staging.log).
 // Ring (1): refill each entry slot as soon as it is consumed, so loads overlap the batch's
 // arithmetic.  Rejected: the kernel is at the 256-VGPR cap, the refills keep the slots live
 // through every consume, and the spills (scratch ops 26 -> 201) cost C3 -33 %, C2 -13 %
