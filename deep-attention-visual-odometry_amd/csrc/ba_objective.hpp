@@ -332,6 +332,8 @@ __device__ __forceinline__ bool ba_eval(const Layout& L, const S* x, const S* d,
   const S cs = tsum / (3.0f * (float)(M - 1));
   const S s = (ps * fN + cs * fM) / fNM;
   const S inv_s = 1.0f / s;
+  // the distorted model's z' == 0 -> 1e-8 (distorted_camera_model.py:57); -0 for the pinhole model
+  const float z_nudge = L.distort ? 1e-8f : -0.0f;
   S ds_over_s = 0.f;
   if constexpr (SLOPE) {
     const S ds = ((sums[1] / (3.0f * fN)) * fN + (tdsum / (3.0f * (float)(M - 1))) * fM) / fNM;
@@ -437,7 +439,9 @@ __device__ __forceinline__ bool ba_eval(const Layout& L, const S* x, const S* d,
       S go0 = 0.f, go1 = 0.f;          // dE/d obs (second-order instantiations only)
       if constexpr (RES == DAVA_RESIDUAL_SQUARED_REPROJECTION) {
         // projection; the distorted model nudges z' == 0 by 1e-8 (distorted_camera_model.py:57)
-        if (DAVA_Z_NUDGE && L.distort && p2 == S(0.0f)) p2 = p2 + 1e-8f;
+        // branch-free: + (-0) leaves every p2 (signed zeros included) bit for bit, so the pinhole
+        // model is untouched; a runtime-uniform branch here cost C2 5% (profiles/r03_ab_c2_regression_bisect.log)
+        if constexpr (DAVA_Z_NUDGE) p2 = p2 + (p2 == S(0.0f) ? z_nudge : -0.0f);
         const S iz = 1.0f / p2;
         const S qx = p0 * iz, qy = p1 * iz;
         const S ub = in.f * qx, vb = in.f * qy;
@@ -605,9 +609,9 @@ __device__ __forceinline__ bool ba_eval(const Layout& L, const S* x, const S* d,
               dp2 = da2 * vc + a2 * dc + k * w2 + Avw * dw2 + e2 * vB + c2 * dB + dtt2;
             }
           }
-          if (DAVA_Z_NUDGE && L.distort) {  // z' == 0 nudge (distorted_camera_model.py:57)
-            if (p2.x == 0.0f) p2.x += 1e-8f;
-            if (p2.y == 0.0f) p2.y += 1e-8f;
+          if constexpr (DAVA_Z_NUDGE) {  // z' == 0 nudge (distorted_camera_model.py:57), branch-free
+            p2.x = p2.x + (p2.x == 0.0f ? z_nudge : -0.0f);
+            p2.y = p2.y + (p2.y == 0.0f ? z_nudge : -0.0f);
           }
           const pf2 iz = 1.0f / p2;
           const pf2 qx = p0 * iz, qy = p1 * iz;
