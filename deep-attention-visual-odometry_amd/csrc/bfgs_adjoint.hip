@@ -49,6 +49,7 @@ struct AdjointArgs {
   float* obs_grad;    // (B, M, N, 2) or null
   float* arows;       // (B, K, Pv) workspace
   int lcap;           // history entries (s_j, w_j), j < lcap, held in LDS for the H passes
+  float* gvws;        // global-vector mode: (B, kAdjGvFloats(Pv)) per-problem vector slices, else null
 };
 
 constexpr int kAdjWaves = 4;
@@ -57,30 +58,37 @@ constexpr int kAdjWaves = 4;
 #endif
 constexpr int kAdjInflight = DAVA_ADJ_INFLIGHT;  // entries per wave in flight in the passes
 constexpr int kAdjBlock = kWave * kAdjWaves;
+constexpr int kAdjMaxGroups = 14;  // GV mode: float4 groups per thread (P <= 14 * 256 * 4 = 14336)
 
 struct AdjointCarve {
   int xb, sbp, gbp, db, gk, p1, p2, wb, sv, wv, yv, gv, ak, an, sc, xd, gd, views, vpart, obs, obsacc, lh, scratch,
       vis_bytes_off, total_bytes;
+  int gv_floats;  // global-vector mode: floats of one problem's workspace slice (the 14 vectors and 2 Dual ones)
 };
 
 // lcap: the oldest history entries' rows (s_j, w_j interleaved) kept on chip for the whole reverse
-// sweep -- every H pass reads them again, so each one held saves 2 Pv floats of HBM per step
-__host__ __device__ inline AdjointCarve carve_adjoint(int M, int N, int Pv, int T, int lcap = 0) {
+// sweep -- every H pass reads them again, so each one held saves 2 Pv floats of HBM per step.
+// gv (global-vector mode, P too large for the LDS image, e.g. C5): the O(P) vectors are offsets into
+// the problem's workspace slice instead, the scene is read in place and the observation cotangent is
+// accumulated straight into the output; LDS keeps the scalars, view constants and reduction scratch.
+__host__ __device__ inline AdjointCarve carve_adjoint(int M, int N, int Pv, int T, int lcap = 0, bool gv = false) {
   AdjointCarve c;
-  int off = 0;
+  int off = 0, voff = 0;
+  int& o = gv ? voff : off;
   int* vec[] = {&c.xb, &c.sbp, &c.gbp, &c.db, &c.gk, &c.p1, &c.p2, &c.wb, &c.sv, &c.wv, &c.yv, &c.gv, &c.ak, &c.an};
-  for (int* v : vec) { *v = off; off += Pv; }
+  for (int* v : vec) { *v = o; o += Pv; }
   c.sc = off; off += T;
-  c.xd = off; off += 2 * Pv;  // Dual
-  c.gd = off; off += 2 * Pv;  // Dual
+  c.xd = o; o += 2 * Pv;  // Dual
+  c.gd = o; o += 2 * Pv;  // Dual
+  c.gv_floats = gv ? voff : 0;
   c.views = off; off += 2 * round_up(views_floats(M), 4);
   c.vpart = off; off += 2 * round_up(vpart_floats(M, kAdjWaves), 4);
-  c.obs = off; off += round_up(2 * M * N, 4);
-  c.obsacc = off; off += round_up(2 * M * N, 4);
-  c.lh = off; off += 2 * lcap * Pv;
+  c.obs = off; off += gv ? 0 : round_up(2 * M * N, 4);
+  c.obsacc = off; off += gv ? 0 : round_up(2 * M * N, 4);
+  c.lh = off; off += gv ? 0 : 2 * lcap * Pv;
   c.scratch = off; off += 2 * kAdjWaves * 32;
   c.vis_bytes_off = off * 4;
-  c.total_bytes = c.vis_bytes_off + round_up(M * N, 16);
+  c.total_bytes = c.vis_bytes_off + (gv ? 0 : round_up(M * N, 16));
   return c;
 }
 
@@ -217,50 +225,135 @@ __device__ __forceinline__ void pair_pass(int P, int Pv, int j0, int j1, const f
   __syncthreads();
 }
 
+// Global-vector mode (rows of up to GT float4 groups per thread, P <= GT * 1024): the same contraction
+// as pair_pass, workgroup-wide.  Thread t owns float4 column groups t, t + 256, ...; v1, v2 and the two
+// running sums stay in registers for the whole pass (one wave per SIMD: up to 512 registers), the rows
+// of E entries are loaded per round, and one block reduction per round gives every thread the entries'
+// dots in the same order.  R1_j0: entry j0's R1 row from this vector instead of R1 + j0 Pv.  out1 / out2
+// may not alias v1 / v2 of another thread's columns (each thread reads and writes only its own).
+template <int GT, class Coef>
+__device__ __forceinline__ void wide_pair_pass(int P, int Pv, int j0, int j1, const float* __restrict__ R1,
+                                               const float* __restrict__ R2, const float* v1, const float* v2,
+                                               float base, Coef coef, float* out1, float* out2, float* scratch,
+                                               int& buf, const float* R1_j0 = nullptr) {
+  constexpr int E = GT <= 8 ? 2 : 1;
+  const int tid = threadIdx.x;
+  const int G = (P + 3) / 4;
+  const f4a z = f4a{0, 0, 0, 0};
+  f4a a[GT], c[GT], pa[GT], pb[GT];
+#pragma unroll
+  for (int u = 0; u < GT; ++u) {
+    const int q = tid + u * kAdjBlock;
+    a[u] = c[u] = pa[u] = pb[u] = z;
+    if (q < G) {
+      a[u] = ldv(v1 + 4 * q);
+      c[u] = ldv(v2 + 4 * q);
+    }
+  }
+  for (int j = j0; j < j1; j += E) {
+    const int ne = min(E, j1 - j);  // uniform
+    f4a r1[E][GT], r2[E][GT];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const float* r1p = (R1_j0 && j + e == j0) ? R1_j0 : R1 + (size_t)(j + e) * Pv;
+      const float* r2p = R2 + (size_t)(j + e) * Pv;
+#pragma unroll
+      for (int u = 0; u < GT; ++u) {
+        const int q = tid + u * kAdjBlock;
+        r1[e][u] = r2[e][u] = z;
+        if (e < ne && q < G) {
+          r1[e][u] = ldv(r1p + 4 * q);
+          r2[e][u] = ldv(r2p + 4 * q);
+        }
+      }
+    }
+    float d[4 * E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      d[4 * e] = d[4 * e + 1] = d[4 * e + 2] = d[4 * e + 3] = 0.f;
+#pragma unroll
+      for (int u = 0; u < GT; ++u) {
+        d[4 * e] += dot4(r1[e][u], a[u]);
+        d[4 * e + 1] += dot4(r2[e][u], a[u]);
+        d[4 * e + 2] += dot4(r1[e][u], c[u]);
+        d[4 * e + 3] += dot4(r2[e][u], c[u]);
+      }
+    }
+    block_sum<4 * E, kAdjWaves>(d, scratch, buf);
+    buf ^= 1;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      if (e < ne) {
+        float k1, k2, k3, k4;
+        coef(j + e, d[4 * e], d[4 * e + 1], d[4 * e + 2], d[4 * e + 3], k1, k2, k3, k4);
+#pragma unroll
+        for (int u = 0; u < GT; ++u) {
+          pa[u] += k1 * r1[e][u] + k2 * r2[e][u];
+          pb[u] += k3 * r1[e][u] + k4 * r2[e][u];
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < GT; ++u) {
+    const int q = tid + u * kAdjBlock;
+    if (q < G) {
+      stv(out1 + 4 * q, pa[u] + base * a[u]);
+      stv(out2 + 4 * q, pb[u] + base * c[u]);
+    }
+  }
+  __syncthreads();
+}
+
 // One workgroup per CU: at two (the C3 image is 78 KB, it would fit) the 256-VGPR cap spills 100-165
 // registers of the dual-number evaluation and the kernel ran 39% slower (148.6 -> 206.9 ms at C3).
-template <int RES, int GM>
+// GT > 0: global-vector mode (the O(P) vectors in the workspace slice a.gvws, wide_pair_pass with up
+// to GT float4 groups per thread); GT = 0: everything O(P) in LDS (pair_pass, GM groups per lane).
+template <int RES, int GM, int GT = 0>
 __global__ __launch_bounds__(kAdjBlock, 1) void bfgs_ba_adjoint_kernel(AdjointArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
+  constexpr bool GVM = GT > 0;
   const Layout L = a.L;
   const int P = L.P, M = L.M, N = L.N, MN = M * N, Pv = a.Pv, K = a.K;
   const int b = blockIdx.x, tid = threadIdx.x;
   const TapeLayout& tl = a.tl;
-  const AdjointCarve cv = carve_adjoint(M, N, Pv, tl.T, a.lcap);
-  float* xb = lds + cv.xb;    // xbar: adjoint of x_{k+1} entering step k, of x_k leaving it
-  float* sbp = lds + cv.sbp;  // adjoint of s_k from the update that used it (step k + 1)
-  float* gbp = lds + cv.gbp;  // adjoint of g_k from y_{k+1} = g_{k+1} - g_k
-  float* db = lds + cv.db;
-  float* gk = lds + cv.gk;
-  float* p1 = lds + cv.p1;
-  float* p2 = lds + cv.p2;
-  float* wb = lds + cv.wb;
+  const AdjointCarve cv = carve_adjoint(M, N, Pv, tl.T, a.lcap, GVM);
+  float* vb = GVM ? a.gvws + (size_t)b * cv.gv_floats : lds;  // base of the O(P) vectors
+  float* xb = vb + cv.xb;    // xbar: adjoint of x_{k+1} entering step k, of x_k leaving it
+  float* sbp = vb + cv.sbp;  // adjoint of s_k from the update that used it (step k + 1)
+  float* gbp = vb + cv.gbp;  // adjoint of g_k from y_{k+1} = g_{k+1} - g_k
+  float* db = vb + cv.db;
+  float* gk = vb + cv.gk;
+  float* p1 = vb + cv.p1;
+  float* p2 = vb + cv.p2;
+  float* wb = vb + cv.wb;
   // H_{k-1} dbar, H_{k-1} wbar: p1 is dead once wbar / sbar are formed, gk until the final loop
   // (which reads hw[i] before it writes gk[i], in the same thread)
   float* hd = p1;
-  float* hw = lds + cv.gk;
-  float* sv = lds + cv.sv;
-  float* wv = lds + cv.wv;
-  float* yv = lds + cv.yv;
-  float* gv = lds + cv.gv;
+  float* hw = vb + cv.gk;
+  float* sv = vb + cv.sv;
+  float* wv = vb + cv.wv;
+  float* yv = vb + cv.yv;
+  float* gv = vb + cv.gv;
   // the passes' cross-wave spares live in the dual vectors' space (dead until the HVP)
-  float* sp0 = lds + cv.xd;
+  float* sp0 = vb + cv.xd;
   float* sp1 = sp0 + Pv;
-  float* sp2 = lds + cv.gd;
+  float* sp2 = vb + cv.gd;
   float* sp3 = sp2 + Pv;
   // a_k lives in LDS while step k updates it (ak) and -wbar_k waits there for step k - 1 (an); the
   // workspace row a_k is written once, final, and only read by later steps (never read-modify-write)
-  float* akl = lds + cv.ak;
-  float* anl = lds + cv.an;
+  float* akl = vb + cv.ak;
+  float* anl = vb + cv.an;
   float* sc = lds + cv.sc;
-  Dual* xd = reinterpret_cast<Dual*>(lds + cv.xd);
-  Dual* gd = reinterpret_cast<Dual*>(lds + cv.gd);
+  Dual* xd = reinterpret_cast<Dual*>(vb + cv.xd);
+  Dual* gd = reinterpret_cast<Dual*>(vb + cv.gd);
   Dual* views = reinterpret_cast<Dual*>(lds + cv.views);
   Dual* vpart = reinterpret_cast<Dual*>(lds + cv.vpart);
-  float* obs = lds + cv.obs;
-  float* obsacc = lds + cv.obsacc;
+  const float* obs = GVM ? a.obs + (size_t)b * 2 * MN : lds + cv.obs;
+  // GV: the observation cotangent is accumulated in place in the output (or not at all)
+  float* obsacc = GVM ? (a.obs_grad ? a.obs_grad + (size_t)b * 2 * MN : nullptr) : lds + cv.obsacc;
   float* scratch = lds + cv.scratch;
-  uint8_t* vis = reinterpret_cast<uint8_t*>(lds) + cv.vis_bytes_off;
+  const uint8_t* vis = GVM ? a.vis + (size_t)b * MN : reinterpret_cast<uint8_t*>(lds) + cv.vis_bytes_off;
 
   const float* S = a.tape + tl.hist + (size_t)b * 2 * tl.kcap * Pv;  // history rows s_j
   const float* W = S + (size_t)tl.kcap * Pv;                          // w_j
@@ -273,23 +366,33 @@ __global__ __launch_bounds__(kAdjBlock, 1) void bfgs_ba_adjoint_kernel(AdjointAr
     sbp[i] = gbp[i] = anl[i] = 0.f;
   }
   for (int i = tid; i < tl.T; i += kAdjBlock) sc[i] = a.tape[tl.scal + (size_t)b * tl.T + i];
-  for (int i = tid; i < 2 * MN; i += kAdjBlock) {
-    obs[i] = a.obs[(size_t)b * 2 * MN + i];
-    obsacc[i] = 0.f;
+  if constexpr (GVM) {
+    if (obsacc)
+      for (int i = tid; i < 2 * MN; i += kAdjBlock) obsacc[i] = 0.f;
+  } else {
+    float* ol = lds + cv.obs;
+    uint8_t* vl = reinterpret_cast<uint8_t*>(lds) + cv.vis_bytes_off;
+    for (int i = tid; i < 2 * MN; i += kAdjBlock) {
+      ol[i] = a.obs[(size_t)b * 2 * MN + i];
+      obsacc[i] = 0.f;
+    }
+    for (int i = tid; i < MN; i += kAdjBlock) vl[i] = a.vis[(size_t)b * MN + i] ? 1 : 0;
   }
-  for (int i = tid; i < MN; i += kAdjBlock) vis[i] = a.vis[(size_t)b * MN + i] ? 1 : 0;
   const int n = min(a.status[(size_t)b * DAVA_STATUS_WORDS], K);
   float* lh = lds + cv.lh;
-  const int nlh = min(a.lcap, max(n - 1, 0));  // history entries 0 .. n-2 exist
+  const int nlh = GVM ? 0 : min(a.lcap, max(n - 1, 0));  // history entries 0 .. n-2 exist
   for (int q = tid; q < nlh * (Pv / 4); q += kAdjBlock) {
     const int j = q / (Pv / 4), i = 4 * (q % (Pv / 4));
     stv(lh + (size_t)2 * j * Pv + i, ldv(S + (size_t)j * Pv + i));
     stv(lh + (size_t)(2 * j + 1) * Pv + i, ldv(W + (size_t)j * Pv + i));
   }
-  const float gamma = sc[3 * K];
   float trace = 0.f;  // sum_{j > k} a_j . g_j with every a_j final (needed at k = 1: gamma's adjoint)
   int buf = 0;
   __syncthreads();
+  // (read after the barrier: sc[3 K] is staged by another thread.  Before it, a thread could read
+  // the slot ahead of its writer -- the LDS image's staging loops usually hid that; in global-vector
+  // mode nothing stands between the two)
+  const float gamma = sc[3 * K];
 
   for (int k = n - 1; k >= 0; --k) {
     const float alpha = sc[k];
@@ -314,11 +417,15 @@ __global__ __launch_bounds__(kAdjBlock, 1) void bfgs_ba_adjoint_kernel(AdjointAr
       __syncthreads();
       const float rho = sc[K + k - 1], c = sc[2 * K + k - 1];
       // P1 = (A + A^T) s, P2 = (A + A^T) w over rows (a_j, g_j), j = k .. n-1
-      pair_pass<GM>(P, Pv, k, n, Ar, Gr, sv, wv, 0.f,
-                    [](int, float as, float gs, float aw, float gw, float& k1, float& k2, float& k3, float& k4) {
-                      k1 = gs; k2 = as; k3 = gw; k4 = aw;
-                    },
-                    p1, p2, sp0, sp1, sp2, sp3, akl);
+      const auto acoef = [](int, float as, float gs, float aw, float gw, float& k1, float& k2, float& k3,
+                            float& k4) {
+        k1 = gs; k2 = as; k3 = gw; k4 = aw;
+      };
+      if constexpr (GVM) {
+        wide_pair_pass<GT>(P, Pv, k, n, Ar, Gr, sv, wv, 0.f, acoef, p1, p2, scratch, buf, akl);
+      } else {
+        pair_pass<GM>(P, Pv, k, n, Ar, Gr, sv, wv, 0.f, acoef, p1, p2, sp0, sp1, sp2, sp3, akl);
+      }
       float r[7] = {0, 0, 0, 0, 0, 0, 0};
       for (int i = tid; i < P; i += kAdjBlock) {
         const float si = sv[i], wi = wv[i], yi = yv[i], di = db[i];
@@ -342,14 +449,14 @@ __global__ __launch_bounds__(kAdjBlock, 1) void bfgs_ba_adjoint_kernel(AdjointAr
       if (k >= 2) {
         const float* hrho = sc + K;
         const float* hc = sc + 2 * K;
-        pair_pass<GM>(P, Pv, 0, k - 1, S, W, db, wb, gamma,
-                      [hrho, hc](int j, float sdv, float wdv, float swv, float wwv, float& k1, float& k2, float& k3,
-                                 float& k4) {
-                        const float rj = hrho[j], cr = hc[j] * rj;
-                        k1 = cr * sdv - rj * wdv; k2 = -rj * sdv;
-                        k3 = cr * swv - rj * wwv; k4 = -rj * swv;
-                      },
-                      hd, hw, sp0, sp1, sp2, sp3, nullptr, lh, nlh);
+        const auto hcoef = [hrho, hc](int j, float sdv, float wdv, float swv, float wwv, float& k1, float& k2,
+                                      float& k3, float& k4) {
+          const float rj = hrho[j], cr = hc[j] * rj;
+          k1 = cr * sdv - rj * wdv; k2 = -rj * sdv;
+          k3 = cr * swv - rj * wwv; k4 = -rj * swv;
+        };
+        if constexpr (GVM) wide_pair_pass<GT>(P, Pv, 0, k - 1, S, W, db, wb, gamma, hcoef, hd, hw, scratch, buf);
+        else pair_pass<GM>(P, Pv, 0, k - 1, S, W, db, wb, gamma, hcoef, hd, hw, sp0, sp1, sp2, sp3, nullptr, lh, nlh);
       } else {
         for (int i = tid; i < Pv; i += kAdjBlock) {
           hd[i] = gamma * db[i];
@@ -405,24 +512,36 @@ __global__ __launch_bounds__(kAdjBlock, 1) void bfgs_ba_adjoint_kernel(AdjointAr
     __syncthreads();
   }
   for (int i = tid; i < P; i += kAdjBlock) a.x0_grad[(size_t)b * P + i] = xb[i];
-  if (a.obs_grad)
+  if (a.obs_grad && !GVM)
     for (int i = tid; i < 2 * MN; i += kAdjBlock) a.obs_grad[(size_t)b * 2 * MN + i] = obsacc[i];
 }
 
 template <int RES>
-static void launch_adjoint(const AdjointArgs& a, int B, int lds, int gm, hipStream_t s) {
+static void launch_adjoint(const AdjointArgs& a, int B, int lds, int gm, int gt, hipStream_t s) {
   auto go = [&](auto kernel) {
     if (lds > 64 * 1024)
       (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     hipLaunchKernelGGL(kernel, dim3(B), dim3(kAdjBlock), lds, s, a);
   };
-  if (gm <= 1) go(bfgs_ba_adjoint_kernel<RES, 1>);
+  if (gt > 0) {  // global-vector mode: 4, 8 or 14 float4 groups per thread
+    if (gt <= 4) go(bfgs_ba_adjoint_kernel<RES, 1, 4>);
+    else if (gt <= 8) go(bfgs_ba_adjoint_kernel<RES, 1, 8>);
+    else go(bfgs_ba_adjoint_kernel<RES, 1, kAdjMaxGroups>);
+  } else if (gm <= 1) go(bfgs_ba_adjoint_kernel<RES, 1>);
   else if (gm == 2) go(bfgs_ba_adjoint_kernel<RES, 2>);
   else if (gm == 3) go(bfgs_ba_adjoint_kernel<RES, 3>);
   else go(bfgs_ba_adjoint_kernel<RES, 4>);
 }
 
 constexpr int kAdjLdsBytes = 160 * 1024;
+
+// Global-vector mode when the LDS image does not fit one CU (or P > 1024, past pair_pass's 4 groups
+// per lane); DAVA_ADJ_FORCE_GV forces it (tests: the same tape through both kernels).
+static bool adjoint_gv(const DavaScene* s, const TapeLayout& tl) {
+  if (getenv("DAVA_ADJ_FORCE_GV")) return true;
+  return s->num_parameters > 1024 || carve_adjoint(s->num_views, s->num_points, tl.Pv, tl.T).total_bytes > kAdjLdsBytes;
+}
+static int adjoint_groups(const TapeLayout& tl) { return (tl.Pv / 4 + kAdjBlock - 1) / kAdjBlock; }
 
 static int adjoint_check(const DavaScene* s, const DavaSolverConfig* c) {
   if (!s || !c) return DAVA_ERR_INVALID_ARGUMENT;
@@ -432,20 +551,34 @@ static int adjoint_check(const DavaScene* s, const DavaSolverConfig* c) {
   if (s->residual != DAVA_RESIDUAL_SQUARED_REPROJECTION && s->residual != DAVA_RESIDUAL_RAY_ANGLE)
     return DAVA_ERR_INVALID_ARGUMENT;
   if (s->residual == DAVA_RESIDUAL_RAY_ANGLE && s->distortion) return DAVA_ERR_UNSUPPORTED;
-  if (c->hessian_mode != DAVA_HESSIAN_COMPACT || c->iterations < 1 || P > 1024) return DAVA_ERR_UNSUPPORTED;
+  if (c->hessian_mode != DAVA_HESSIAN_COMPACT || c->iterations < 1 || c->iterations > 1025) return DAVA_ERR_UNSUPPORTED;
   const TapeLayout tl = tape_layout(s->batch, P, c->iterations);
-  if (carve_adjoint(s->num_views, s->num_points, tl.Pv, tl.T).total_bytes > kAdjLdsBytes) return DAVA_ERR_UNSUPPORTED;
+  if (adjoint_gv(s, tl)) {
+    if (adjoint_groups(tl) > kAdjMaxGroups) return DAVA_ERR_UNSUPPORTED;
+    if (carve_adjoint(s->num_views, s->num_points, tl.Pv, tl.T, 0, true).total_bytes > kAdjLdsBytes)
+      return DAVA_ERR_UNSUPPORTED;
+  }
   return DAVA_OK;
 }
 
 // As many history entries on chip as the CU's LDS leaves room for (one workgroup per CU), at most
-// the K - 1 a solve can make; DAVA_ADJ_LDS_ENTRIES caps it (0: none) for A/B runs.
+// the K - 1 a solve can make; DAVA_ADJ_LDS_ENTRIES caps it (0: none) for A/B runs.  None in GV mode.
 static int adjoint_lds_entries(const DavaScene* s, const TapeLayout& tl) {
+  if (adjoint_gv(s, tl)) return 0;
   const int base = carve_adjoint(s->num_views, s->num_points, tl.Pv, tl.T).total_bytes;
   int n = (kAdjLdsBytes - base) / (int)(2 * tl.Pv * sizeof(float));
   n = max(0, min(n, tl.K - 1));
   if (const char* e = getenv("DAVA_ADJ_LDS_ENTRIES")) n = max(0, min(n, atoi(e)));
   return n;
+}
+
+// workspace: the a rows (B, K, Pv), then in GV mode the per-problem vector slices
+static size_t adjoint_rows_bytes(const DavaScene* s, const TapeLayout& tl) {
+  return (size_t)s->batch * tl.K * tl.Pv * sizeof(float);
+}
+static size_t adjoint_gv_bytes(const DavaScene* s, const TapeLayout& tl) {
+  if (!adjoint_gv(s, tl)) return 0;
+  return (size_t)s->batch * carve_adjoint(s->num_views, s->num_points, tl.Pv, tl.T, 0, true).gv_floats * sizeof(float);
 }
 
 }  // namespace dava
@@ -455,7 +588,7 @@ using namespace dava;
 extern "C" size_t dava_ba_solve_backward_workspace_bytes(const DavaScene* scene, const DavaSolverConfig* config) {
   if (adjoint_check(scene, config) != DAVA_OK) return 0;
   const TapeLayout tl = tape_layout(scene->batch, scene->num_parameters, config->iterations);
-  return (size_t)scene->batch * tl.K * tl.Pv * sizeof(float) + 256;
+  return adjoint_rows_bytes(scene, tl) + adjoint_gv_bytes(scene, tl) + 256;
 }
 
 extern "C" int dava_ba_solve_backward_lds_entries(const DavaScene* scene, const DavaSolverConfig* config) {
@@ -474,7 +607,9 @@ extern "C" int dava_ba_solve_backward(const DavaScene* scene, const DavaSolverCo
     return DAVA_ERR_INVALID_ARGUMENT;
   const TapeLayout tl = tape_layout(scene->batch, scene->num_parameters, config->iterations);
   if (tape_bytes < tl.queue_byte) return DAVA_ERR_WORKSPACE;
-  if (!workspace || workspace_bytes < (size_t)scene->batch * tl.K * tl.Pv * sizeof(float)) return DAVA_ERR_WORKSPACE;
+  const size_t rows = adjoint_rows_bytes(scene, tl), gvb = adjoint_gv_bytes(scene, tl);
+  if (!workspace || workspace_bytes < rows + gvb) return DAVA_ERR_WORKSPACE;
+  const bool gv = adjoint_gv(scene, tl);
   AdjointArgs a;
   a.L = Layout{scene->num_views, scene->num_points, scene->num_parameters, scene->distortion ? 1 : 0};
   a.Pv = tl.Pv;
@@ -488,11 +623,13 @@ extern "C" int dava_ba_solve_backward(const DavaScene* scene, const DavaSolverCo
   a.x0_grad = x0_grad;
   a.obs_grad = observations_grad;
   a.arows = static_cast<float*>(workspace);
+  a.gvws = gv ? reinterpret_cast<float*>(static_cast<char*>(workspace) + rows) : nullptr;
   a.lcap = adjoint_lds_entries(scene, tl);
-  const int lds = carve_adjoint(scene->num_views, scene->num_points, tl.Pv, tl.T, a.lcap).total_bytes;
+  const int lds = carve_adjoint(scene->num_views, scene->num_points, tl.Pv, tl.T, a.lcap, gv).total_bytes;
   const int gm = (tl.Pv / 4 + kWave - 1) / kWave;
+  const int gt = gv ? adjoint_groups(tl) : 0;
   hipStream_t s = static_cast<hipStream_t>(stream);
-  if (scene->residual == DAVA_RESIDUAL_RAY_ANGLE) launch_adjoint<DAVA_RESIDUAL_RAY_ANGLE>(a, scene->batch, lds, gm, s);
-  else launch_adjoint<DAVA_RESIDUAL_SQUARED_REPROJECTION>(a, scene->batch, lds, gm, s);
+  if (scene->residual == DAVA_RESIDUAL_RAY_ANGLE) launch_adjoint<DAVA_RESIDUAL_RAY_ANGLE>(a, scene->batch, lds, gm, gt, s);
+  else launch_adjoint<DAVA_RESIDUAL_SQUARED_REPROJECTION>(a, scene->batch, lds, gm, gt, s);
   return hipGetLastError() == hipSuccess ? DAVA_OK : DAVA_ERR_LAUNCH;
 }

@@ -56,6 +56,7 @@ struct SolveArgs {
   int stagger_levels;  // <= 1: odd workgroups wait `stagger`; L > 1: level (b / 8) mod L waits level x stagger
   float drop_p;   // training-mode drop path probability (0: eval mode)
   unsigned long long drop_seed;
+  int second_last;  // training mode's return_second_last: a minimum-step stop keeps x_k
 };
 
 // Training mode's drop path (bfgs_solver.py:121-125): problem b keeps updating at iteration k iff
@@ -176,6 +177,9 @@ __device__ __forceinline__ void st4(float* p, float4 v) { *reinterpret_cast<floa
 #endif
 #ifndef DAVA_TRIAL_DOT
 #define DAVA_TRIAL_DOT 0  // 1: trial slope as d . grad (reverse mode); 0: forward-mode JVP
+#endif
+#ifndef DAVA_TRIAL_DOT_GV
+#define DAVA_TRIAL_DOT_GV 1  // global-vector mode: slope from the gradient (C5 +4%, profiles/r03_ab_c5_dot_hyd.log)
 #endif
 #ifndef DAVA_TRIAL_CHECK
 #define DAVA_TRIAL_CHECK 1  // skip evaluating trial points that round back to x
@@ -494,6 +498,16 @@ __device__ __forceinline__ void compact_products_wide(int P, int Pv, int nh, con
 // profiles/r03_ab_c5_park_yg_lds.log: parking y and g in the dead LDS gradient / direction slots to
 // free registers for two entries per reduction -- bitwise equal, but the per-entry LDS re-reads and
 // the spills cost 14% with one entry and 19% with two.)
+// HYD (DAVA_HY_FROM_D): only H'g is formed from the history; H'y = H'g - H'g_prev = H'g + d_prev,
+// since the previous direction was d_prev = -H' g_prev (H' = H_{k-1} in both).  Two dots and one
+// accumulation per entry instead of four and two, and y / H'y leave the registers, which holds
+// DAVA_GV_ENTRIES_HYD entries per block reduction instead of one.  Same bytes; different rounding.
+#ifndef DAVA_HY_FROM_D
+#define DAVA_HY_FROM_D 0
+#endif
+#ifndef DAVA_GV_ENTRIES_HYD
+#define DAVA_GV_ENTRIES_HYD 2
+#endif
 template <int GT, int NW>
 __device__ __forceinline__ float wide_direction(int P, int Pv, int nh, const float* __restrict__ S,
                                                 const float* __restrict__ W, float* hrho, float* hc, float gamma0,
@@ -501,7 +515,9 @@ __device__ __forceinline__ float wide_direction(int P, int Pv, int nh, const flo
                                                 float* s_row, float* w_row, float* scratch, int& buf, int entry,
                                                 float* tape_rho, float* tape_c) {
   constexpr int BLOCK = kWave * NW;
-  constexpr int E = GT <= 2 ? 2 : DAVA_GV_ENTRIES;
+  constexpr bool HYD = DAVA_HY_FROM_D;
+  constexpr int E = HYD ? (GT <= 2 ? 4 : DAVA_GV_ENTRIES_HYD) : (GT <= 2 ? 2 : DAVA_GV_ENTRIES);
+  constexpr int ND = HYD ? 2 : 4;  // dots per entry
   const int tid = threadIdx.x;
   const int G = (P + 3) / 4;
   const f4v z = f4v{0, 0, 0, 0};
@@ -512,10 +528,61 @@ __device__ __forceinline__ float wide_direction(int P, int Pv, int nh, const flo
     y[u] = gg[u] = pa[u] = pb[u] = z;
     if (q < G) {
       gg[u] = *reinterpret_cast<const f4v*>(g + 4 * q);
-      y[u] = gg[u] - *reinterpret_cast<const f4v*>(gp + 4 * q);
+      if constexpr (!HYD) y[u] = gg[u] - *reinterpret_cast<const f4v*>(gp + 4 * q);
     }
   }
-  for (int j = 0; j < nh; j += E) {
+  if constexpr (HYD) {
+    for (int j = 0; j < nh; j += E) {
+      const int ne = min(E, nh - j);  // uniform
+      f4v s4[E][GT], w4[E][GT];
+      float dd[ND * E];
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+#pragma unroll
+        for (int u = 0; u < GT; ++u) {
+          const int q = tid + u * BLOCK;
+          s4[e][u] = w4[e][u] = z;
+          if (e < ne && q < G) {
+            s4[e][u] = *reinterpret_cast<const f4v*>(S + (size_t)(j + e) * Pv + 4 * q);
+            w4[e][u] = *reinterpret_cast<const f4v*>(W + (size_t)(j + e) * Pv + 4 * q);
+          }
+        }
+      }
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        f2v sg2 = {0.f, 0.f}, wg2 = {0.f, 0.f};
+#pragma unroll
+        for (int u = 0; u < GT; ++u) {
+          sg2 = pk_fma(s4[e][u].lo, gg[u].lo, sg2); sg2 = pk_fma(s4[e][u].hi, gg[u].hi, sg2);
+          wg2 = pk_fma(w4[e][u].lo, gg[u].lo, wg2); wg2 = pk_fma(w4[e][u].hi, gg[u].hi, wg2);
+        }
+        dd[ND * e] = sg2.x + sg2.y;
+        dd[ND * e + 1] = wg2.x + wg2.y;
+      }
+      block_sum<ND * E, NW>(dd, scratch, buf);
+      buf ^= 1;
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        if (e < ne) {
+          const float rho = hrho[j + e], cr = hc[j + e] * rho;
+          const float ag = fmaf(cr, dd[ND * e], -(rho * dd[ND * e + 1])), bg = -rho * dd[ND * e];
+#pragma unroll
+          for (int u = 0; u < GT; ++u) pb[u] = pk_fma4(bg, w4[e][u], pk_fma4(ag, s4[e][u], pb[u]));
+        }
+      }
+    }
+    // H'g = sum + gamma0 g;  H'y = H'g + d_prev (d still holds the previous direction);  y = g - g_prev
+#pragma unroll
+    for (int u = 0; u < GT; ++u) {
+      const int q = tid + u * BLOCK;
+      pb[u] += gamma0 * gg[u];
+      if (q < G) {
+        pa[u] = pb[u] + *reinterpret_cast<const f4v*>(d + 4 * q);
+        y[u] = gg[u] - *reinterpret_cast<const f4v*>(gp + 4 * q);
+      }
+    }
+  }
+  for (int j = 0; j < (HYD ? 0 : nh); j += E) {
     const int ne = min(E, nh - j);  // uniform
     f4v s4[E][GT], w4[E][GT];
     float dd[4 * E];
@@ -591,8 +658,10 @@ __device__ __forceinline__ float wide_direction(int P, int Pv, int nh, const flo
   for (int u = 0; u < GT; ++u) {
     const int q = tid + u * BLOCK;
     const f4v yu = y[u], gu = gg[u];
-    pa[u] += gamma0 * yu;
-    pb[u] += gamma0 * gu;
+    if constexpr (!HYD) {
+      pa[u] += gamma0 * yu;
+      pb[u] += gamma0 * gu;
+    }
     sv[u] = q < G ? *reinterpret_cast<const f4v*>(s_cur + 4 * q) : z;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
@@ -903,6 +972,7 @@ __global__ __launch_bounds__(kWave * NW, DAVA_SOLVE_WAVES_PER_EU) void bfgs_ba_s
   static_assert(!XL || GV, "XL is a global-vector-mode variant");
   static_assert(GV ? NW == solve_waves(true) : (NW == 1 || NW == 2 || NW == 4), "LDS mode runs 1-, 2- or 4-wave workgroups");
   constexpr int BLOCK = kWave * NW;
+  constexpr bool kTrialDot = GV ? DAVA_TRIAL_DOT_GV : DAVA_TRIAL_DOT;
   extern __shared__ __attribute__((aligned(16))) float lds[];
 #if DAVA_BASE_PRIO
   __builtin_amdgcn_s_setprio(DAVA_BASE_PRIO);
@@ -1229,7 +1299,7 @@ __global__ __launch_bounds__(kWave * NW, DAVA_SOLVE_WAVES_PER_EU) void bfgs_ba_s
         // next iterate's gradient) and phi'(alpha) = d . grad (DOT).
         const bool known_same = DAVA_TRIAL_CHECK && al <= nomove_al;  // uniform
         if (!known_same &&
-            ba_eval<true, !DAVA_TRIAL_DOT, true, DAVA_TRIAL_DOT, DAVA_TRIAL_CHECK, RES, float, NW, PPT,
+            ba_eval<true, !kTrialDot, true, kTrialDot, DAVA_TRIAL_CHECK, RES, float, NW, PPT,
                     GV && DAVA_PACKED_PAIRS>(
                 L, x, d, al, obs, vis, grad_buf(gp), views, vpart, scratch, buf, fa, dfa)) {
           ++evals;
@@ -1307,16 +1377,28 @@ __global__ __launch_bounds__(kWave * NW, DAVA_SOLVE_WAVES_PER_EU) void bfgs_ba_s
       // ---- take the step (bfgs_solver.py:191-199) and test its length (:203-207) ----
       {
         float r[1] = {0.f};
-        for (int i = tid; i < P; i += BLOCK) {
-          const float si = __fmul_rn(alpha, d[i]);
-          s_cur[i] = si;
-          x[i] = __fadd_rn(x[i], si);
-          r[0] += si * si;
+        if (a.second_last) {  // x moves only once the step has passed the test (uniform branch)
+          for (int i = tid; i < P; i += BLOCK) {
+            const float si = __fmul_rn(alpha, d[i]);
+            s_cur[i] = si;
+            r[0] += si * si;
+          }
+        } else {
+          for (int i = tid; i < P; i += BLOCK) {
+            const float si = __fmul_rn(alpha, d[i]);
+            s_cur[i] = si;
+            x[i] = __fadd_rn(x[i], si);
+            r[0] += si * si;
+          }
         }
         block_sum<1, NW>(r, scratch, buf); buf ^= 1;
         ++steps;
         DAVA_PHASE(5);
         if (!(sqrtf(r[0]) > a.min_step)) { reason = DAVA_STOP_STEP; break; }
+        if (a.second_last) {  // the same additions, after the test (bfgs_solver.py:208-212)
+          for (int i = tid; i < P; i += BLOCK) x[i] = __fadd_rn(x[i], s_cur[i]);
+          __syncthreads();
+        }
       }
     }
     if (k == kend && kend < a.iters) reason = DAVA_STOP_DROP;  // uniform
@@ -1610,12 +1692,22 @@ static void launch_solve(const SolveArgs& a, int B, int lds, hipStream_t s, int 
   else launch_solve_res<MODE, GV, DAVA_RESIDUAL_SQUARED_REPROJECTION, XL>(a, B, lds, s, nw);
 }
 
-// A recording solve (the tape of dava_tape.hpp) needs COMPACT mode with the O(P) state in LDS and
-// rows of at most 4 x 64 float4 groups (P <= 1024), the shapes the adjoint kernel implements.
+// A recording solve (the tape of dava_tape.hpp) needs COMPACT mode and P <= 14336: the adjoint kernel
+// runs P <= 1024 with its O(P) vectors in LDS and larger P (the forward's global-vector mode, e.g. C5)
+// with them in its workspace, both over rows of at most 14 float4 groups per thread.  A GV-mode
+// recording also needs the forward's wide single-pass history products (the ones that write the tape).
+constexpr int kTapeMaxParameters = 14336;
 static bool tape_supported(const DavaScene* scene, const DavaSolverConfig* config) {
   if (config->hessian_mode != DAVA_HESSIAN_COMPACT || config->iterations < 1) return false;
   const int kcap = compact_capacity(config);
-  return kcap <= kMaxCompactEntries && !use_gv(scene, kcap) && scene->num_parameters <= 1024;
+  if (kcap > kMaxCompactEntries || scene->num_parameters > kTapeMaxParameters) return false;
+  const bool gv = use_gv(scene, kcap);
+  return !gv || wide_history_pass(round_up(scene->num_parameters, 4), kcap, true);
+}
+static TapeLayout solve_tape_layout(const DavaScene* scene, const DavaSolverConfig* config) {
+  const int kcap = compact_capacity(config);
+  const int Pv = round_up(scene->num_parameters, 4);
+  return tape_layout(scene->batch, scene->num_parameters, config->iterations, use_gv(scene, kcap) ? kVectors * Pv : 0);
 }
 
 static int solve_impl(const DavaScene* scene, const DavaSolverConfig* config, const float* x0, float* x_out,
@@ -1640,7 +1732,7 @@ static int solve_impl(const DavaScene* scene, const DavaSolverConfig* config, co
   const int lds = lds_bytes_for(scene, kcap, gv, lcap, xl, nw);
   if (lds > kMaxLds) return DAVA_ERR_UNSUPPORTED;
   const size_t vec = gv ? gv_vector_bytes(scene) : 0;
-  const TapeLayout tl = tape_layout(scene->batch, scene->num_parameters, config->iterations);
+  const TapeLayout tl = solve_tape_layout(scene, config);
   const size_t need = record ? tl.queue_byte : solve_state_bytes(scene, config);
   const bool uses_ws = record || gv || (mode == DAVA_HESSIAN_DENSE ? config->iterations > 2 : config->iterations > 1);
   if (uses_ws && (!workspace || workspace_bytes < need)) return DAVA_ERR_WORKSPACE;
@@ -1675,6 +1767,7 @@ static int solve_impl(const DavaScene* scene, const DavaSolverConfig* config, co
   a.stagger_levels = 1;
   a.drop_p = config->drop_path_p;
   a.drop_seed = ((unsigned long long)config->drop_seed_hi << 32) | config->drop_seed_lo;
+  a.second_last = config->return_second_last ? 1 : 0;
   a.queue = queue ? reinterpret_cast<int*>(static_cast<char*>(workspace) + need) : nullptr;
   a.tape_x = a.tape_g = a.tape_s = nullptr;
   a.tape_T = tl.T;
@@ -1684,6 +1777,7 @@ static int solve_impl(const DavaScene* scene, const DavaSolverConfig* config, co
     a.tape_x = t + tl.x;
     a.tape_g = t + tl.g;
     a.tape_s = t + tl.scal;
+    a.vecs = gv ? t + tl.vecs : nullptr;
   }
   hipStream_t s = static_cast<hipStream_t>(stream);
   // (a recording zeroes its whole queue tail: the tape tensor handed back includes it)
@@ -1750,7 +1844,7 @@ extern "C" int dava_ba_solve(const DavaScene* scene, const DavaSolverConfig* con
 
 extern "C" size_t dava_ba_solve_tape_bytes(const DavaScene* scene, const DavaSolverConfig* config) {
   if (check_scene(scene, false) != DAVA_OK || !config || !tape_supported(scene, config)) return 0;
-  return tape_layout(scene->batch, scene->num_parameters, config->iterations).total_bytes;
+  return solve_tape_layout(scene, config).total_bytes;
 }
 
 extern "C" int dava_ba_solve_record(const DavaScene* scene, const DavaSolverConfig* config, const float* x0,

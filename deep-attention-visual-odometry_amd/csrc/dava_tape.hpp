@@ -10,6 +10,8 @@
 //   g      (B, K, Pv)        g_k = dE/dx (x_k)
 //   scal   (B, T)            [alpha_0..alpha_{K-1} | rho_0..rho_{K-1} | c_0..c_{K-1} | gamma],
 //                            T = round_up(3 K + 1, 4)
+//   vecs   (B, V)            global-vector-mode recordings only: the solve's O(P) vectors (V floats per
+//                            problem, scratch of the recording launch; the adjoint does not read them)
 //   queue  256 bytes          the work-queue counter of the recording launch
 #pragma once
 
@@ -19,13 +21,13 @@ namespace dava {
 
 struct TapeLayout {
   int K, kcap, Pv, T;
-  size_t hist, x, g, scal;  // offsets in floats
+  size_t hist, x, g, scal, vecs;  // offsets in floats
   size_t queue_byte, total_bytes;
 };
 
 inline int tape_round_up(int v, int m) { return (v + m - 1) / m * m; }
 
-inline TapeLayout tape_layout(int B, int P, int K) {
+inline TapeLayout tape_layout(int B, int P, int K, int vec_floats = 0) {
   TapeLayout t;
   t.K = K > 0 ? K : 1;
   t.kcap = K > 1 ? K - 1 : 1;
@@ -36,7 +38,8 @@ inline TapeLayout tape_layout(int B, int P, int K) {
   t.x = t.hist + b * 2 * (size_t)t.kcap * t.Pv;
   t.g = t.x + b * (size_t)t.K * t.Pv;
   t.scal = t.g + b * (size_t)t.K * t.Pv;
-  t.queue_byte = (t.scal + b * (size_t)t.T) * sizeof(float);
+  t.vecs = t.scal + b * (size_t)t.T;
+  t.queue_byte = (t.vecs + b * (size_t)(vec_floats > 0 ? vec_floats : 0)) * sizeof(float);
   t.total_bytes = t.queue_byte + 256;
   return t;
 }

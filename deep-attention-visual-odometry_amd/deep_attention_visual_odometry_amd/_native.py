@@ -20,7 +20,7 @@ DAVA_HESSIAN_DENSE = 0
 DAVA_HESSIAN_COMPACT = 1
 DAVA_RESIDUAL_SQUARED_REPROJECTION = 0
 DAVA_RESIDUAL_RAY_ANGLE = 1
-ABI_VERSION = 3  # include/dava_ba.h DAVA_ABI_VERSION
+ABI_VERSION = 4  # include/dava_ba.h DAVA_ABI_VERSION
 STOP_ITERATIONS, STOP_ERROR, STOP_STEP, STOP_DROP = 0, 1, 2, 3
 STATUS_WORDS = 4
 
@@ -55,6 +55,7 @@ class DavaSolverConfig(ctypes.Structure):
         ("drop_path_p", ctypes.c_float),
         ("drop_seed_lo", ctypes.c_uint32),
         ("drop_seed_hi", ctypes.c_uint32),
+        ("return_second_last", _c_i32),
     ]
 
 

@@ -47,11 +47,13 @@ def scene_struct(observations: Optional[Tensor], visibility: Optional[Tensor], n
 
 
 def solver_config(sufficient_decrease, curvature, error_threshold, iterations, minimum_step, max_line_search_trials,
-                  strong, hessian_mode, drop_path_p: float = 0.0, drop_seed: int = 0) -> N.DavaSolverConfig:
+                  strong, hessian_mode, drop_path_p: float = 0.0, drop_seed: int = 0,
+                  return_second_last: bool = False) -> N.DavaSolverConfig:
     seed = int(drop_seed) & 0xFFFFFFFFFFFFFFFF
     return N.DavaSolverConfig(float(sufficient_decrease), float(curvature), float(error_threshold),
                               float(minimum_step), int(iterations), int(max_line_search_trials),
-                              1 if strong else 0, int(hessian_mode), float(drop_path_p), seed & 0xFFFFFFFF, seed >> 32)
+                              1 if strong else 0, int(hessian_mode), float(drop_path_p), seed & 0xFFFFFFFF, seed >> 32,
+                              1 if return_second_last else 0)
 
 
 def _check_scene_tensors(x: Tensor, observations: Tensor, visibility: Tensor, num_views: int, num_points: int,
@@ -79,7 +81,7 @@ def ba_solve(x0: Tensor, observations: Tensor, visibility: Tensor, num_views: in
              distortion: bool, sufficient_decrease: float, curvature: float, error_threshold: float,
              iterations: int, minimum_step: float, max_line_search_trials: int, strong: bool, hessian_mode: int,
              residual: int, want_error: bool, workspace: Tensor, drop_path_p: float = 0.0,
-             drop_seed: int = 0) -> Tuple[Tensor, Tensor, Tensor]:
+             drop_seed: int = 0, return_second_last: bool = False) -> Tuple[Tensor, Tensor, Tensor]:
     """``dava_ba_solve``: the whole eval-mode BFGS solve of a (B, P) fp32 batch in one launch.
     ``workspace``: a uint8 scratch buffer of at least ``dava_ba_solve_workspace_bytes`` (its contents
     are overwritten), or an empty tensor to allocate one per call.
@@ -90,7 +92,7 @@ def ba_solve(x0: Tensor, observations: Tensor, visibility: Tensor, num_views: in
     dev = x0.device
     sc = scene_struct(observations, visibility, num_views, num_points, distortion, b, residual)
     cfg = solver_config(sufficient_decrease, curvature, error_threshold, iterations, minimum_step,
-                        max_line_search_trials, strong, hessian_mode, drop_path_p, drop_seed)
+                        max_line_search_trials, strong, hessian_mode, drop_path_p, drop_seed, return_second_last)
     need = int(lib.dava_ba_solve_workspace_bytes(sc, cfg))
     if workspace.numel() < need or workspace.device != dev or workspace.dtype != torch.uint8:
         if workspace.numel() > 0:
@@ -109,7 +111,7 @@ def ba_solve(x0: Tensor, observations: Tensor, visibility: Tensor, num_views: in
 @ba_solve.register_fake
 def _(x0, observations, visibility, num_views, num_points, distortion, sufficient_decrease, curvature,
       error_threshold, iterations, minimum_step, max_line_search_trials, strong, hessian_mode, residual, want_error,
-      workspace, drop_path_p=0.0, drop_seed=0):
+      workspace, drop_path_p=0.0, drop_seed=0, return_second_last=False):
     b = x0.shape[0]
     return (torch.empty_like(x0), x0.new_empty((b,) if want_error else (0,)),
             x0.new_empty((b, N.STATUS_WORDS), dtype=torch.int32))
@@ -210,7 +212,8 @@ def _(x, observations, visibility, num_views, num_points, distortion, direction,
 def ba_solve_record(x0: Tensor, observations: Tensor, visibility: Tensor, num_views: int, num_points: int,
                     distortion: bool, sufficient_decrease: float, curvature: float, error_threshold: float,
                     iterations: int, minimum_step: float, max_line_search_trials: int, strong: bool,
-                    residual: int, drop_path_p: float = 0.0, drop_seed: int = 0) -> Tuple[Tensor, Tensor, Tensor]:
+                    residual: int, drop_path_p: float = 0.0, drop_seed: int = 0,
+                    return_second_last: bool = False) -> Tuple[Tensor, Tensor, Tensor]:
     """``dava_ba_solve_record``: the fused COMPACT solve (bitwise ``ba_solve``'s x and status) plus the
     tape the adjoint replays.  Returns (x, status (B, 4) int32, tape uint8)."""
     lib = N.load_library()
@@ -218,11 +221,12 @@ def ba_solve_record(x0: Tensor, observations: Tensor, visibility: Tensor, num_vi
     b, dev = x0.shape[0], x0.device
     sc = scene_struct(observations, visibility, num_views, num_points, distortion, b, residual)
     cfg = solver_config(sufficient_decrease, curvature, error_threshold, iterations, minimum_step,
-                        max_line_search_trials, strong, N.DAVA_HESSIAN_COMPACT, drop_path_p, drop_seed)
+                        max_line_search_trials, strong, N.DAVA_HESSIAN_COMPACT, drop_path_p, drop_seed,
+                        return_second_last)
     need = int(lib.dava_ba_solve_tape_bytes(sc, cfg))
     if need == 0:
-        raise ValueError("this scene / configuration has no fused adjoint (compact mode, P <= 1024, "
-                         "iterations >= 1, the O(P) state in LDS)")
+        raise ValueError("this scene / configuration has no fused adjoint (compact mode, P <= 14336, "
+                         "iterations >= 1)")
     tape = torch.empty(need, dtype=torch.uint8, device=dev)
     if _POISON:  # debugging aid: every byte the kernels do not write reads back as NaN
         tape.fill_(0xFF)
@@ -237,7 +241,7 @@ def ba_solve_record(x0: Tensor, observations: Tensor, visibility: Tensor, num_vi
 @ba_solve_record.register_fake
 def _(x0, observations, visibility, num_views, num_points, distortion, sufficient_decrease, curvature,
       error_threshold, iterations, minimum_step, max_line_search_trials, strong, residual, drop_path_p=0.0,
-      drop_seed=0):
+      drop_seed=0, return_second_last=False):
     b = x0.shape[0]
     ctx = torch.library.get_ctx()
     return (torch.empty_like(x0), x0.new_empty((b, N.STATUS_WORDS), dtype=torch.int32),

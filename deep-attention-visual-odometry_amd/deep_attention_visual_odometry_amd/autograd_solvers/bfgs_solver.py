@@ -24,6 +24,10 @@ line search is detached, as in the reference.  A fused objective
 double backward is the forward-over-reverse kernel (H v and the observation
 cross term, csrc/ba_second_order.hip), so gradients reach captured observations.
 
+Training mode's ``return_second_last`` runs fused too (a problem stopped by the minimum-step rule
+keeps x before its last step); when the reference's scatter would have moved rows between problems
+(``native_ops.second_last_moves_rows``) the solve is redone by the generic loop, which reproduces it.
+
 Not supported (raises rather than silently falling back): CPU tensors.
 """
 import os
@@ -100,18 +104,23 @@ class BFGSSolver(Module):
             error_threshold, num_iterations = self.training_error_threshold, self.training_iterations
         else:
             error_threshold, num_iterations = self.error_threshold, self.iterations
-        # training mode's drop path runs fused (counter-based draws, DAVA_STOP_DROP); the reference's
-        # return_second_last scatter (:196-212) moves rows between problems, so it stays generic
+        # training mode's drop path runs fused (counter-based draws, DAVA_STOP_DROP), and so does
+        # return_second_last (:196-212) unless the reference's scatter would move rows between problems
         drop_p = self.drop_path_p if self.training else 0.0
+        second_last = self.training and self.return_second_last
         generic_training = drop_p > 0.0 and bool(os.environ.get("DAVA_GENERIC_TRAINING"))  # torch-RNG generic loop
-        if isinstance(error_function, ReprojectionError) and not (self.training and self.return_second_last) \
-                and not generic_training:
+        if isinstance(error_function, ReprojectionError) and not generic_training:
             seed = int(torch.randint(0, 2 ** 62, (1,)).item()) if drop_p > 0.0 else 0  # from torch's default generator
+            out = None
             if not parameters.requires_grad:
-                return self._fused(parameters, error_function, error_threshold, num_iterations, drop_p, seed)
-            if self._adjoint_available(parameters, error_function, num_iterations):
-                return self._fused_differentiable(parameters, error_function, error_threshold, num_iterations,
-                                                  drop_p, seed)
+                out = self._fused(parameters, error_function, error_threshold, num_iterations, drop_p, seed,
+                                  second_last)
+            elif self._adjoint_available(parameters, error_function, num_iterations):
+                out = self._fused_differentiable(parameters, error_function, error_threshold, num_iterations,
+                                                 drop_p, seed, second_last)
+            if out is not None and not (second_last and native_ops.second_last_moves_rows(self.last_status)):
+                return out
+            self.last_status = None  # the generic loop below has no status words
         if isinstance(error_function, ReprojectionError):
             self._check_generic_fits(parameters, num_iterations)
         return self._generic(parameters, error_function, error_threshold, num_iterations)
@@ -133,13 +142,14 @@ class BFGSSolver(Module):
                     else "training mode with return_second_last")
             raise RuntimeError(
                 f"{what} at B={b}, P={p}, {num_iterations} iterations has no fused kernel here (the adjoint covers "
-                f"compact mode with P <= 1024 and at most {self.MAX_COMPACT_ENTRIES + 1} iterations); the generic "
+                f"compact mode with P <= 14336 and at most {self.MAX_COMPACT_ENTRIES + 1} iterations); the generic "
                 f"loop would hold the dense (B, P, P) inverse Hessian ~{need / 2 ** 30:.0f} GiB against "
                 f"{free / 2 ** 30:.0f} GiB free. Reduce the batch or the iteration count.")
 
     def _adjoint_available(self, parameters, fn: ReprojectionError, num_iterations) -> bool:
         """Differentiating through a fused objective's solve runs the recording solve + adjoint
-        kernel (compact history; C1-C3 shapes) unless dense mode was asked for or
+        kernel (compact history; P <= 14336: C1-C3 with the O(P) vectors in LDS, C5 with them in
+        HBM) unless dense mode was asked for or
         DAVA_GENERIC_BACKWARD is set (then: the generic loop, graph kept by torch)."""
         if self.hessian_mode == "dense" or os.environ.get("DAVA_GENERIC_BACKWARD"):
             return False
@@ -149,7 +159,7 @@ class BFGSSolver(Module):
                                                fn.num_points, fn.distortion, num_iterations, fn.residual)
 
     def _fused_differentiable(self, parameters, fn: ReprojectionError, error_threshold, num_iterations, drop_p=0.0,
-                              seed=0):
+                              seed=0, second_last=False):
         lead = parameters.shape[:-1]
         if fn.batch_shape != lead:
             raise ValueError(f"ReprojectionError batch shape {tuple(fn.batch_shape)} != parameters {tuple(lead)}")
@@ -159,11 +169,12 @@ class BFGSSolver(Module):
             fn.visibility.reshape(-1, fn.num_views, fn.num_points), fn.num_views, fn.num_points, fn.distortion,
             sufficient_decrease=self.sufficient_decrease, curvature=self.curvature, error_threshold=error_threshold,
             iterations=num_iterations, minimum_step=self.minimum_step, residual=fn.residual, drop_path_p=drop_p,
-            drop_seed=seed)
+            drop_seed=seed, return_second_last=second_last)
         self.last_status = status
         return x.reshape(parameters.shape)
 
-    def _fused(self, parameters, fn: ReprojectionError, error_threshold, num_iterations, drop_p=0.0, seed=0):
+    def _fused(self, parameters, fn: ReprojectionError, error_threshold, num_iterations, drop_p=0.0, seed=0,
+               second_last=False):
         lead = parameters.shape[:-1]
         if fn.batch_shape != lead:
             raise ValueError(f"ReprojectionError batch shape {tuple(fn.batch_shape)} != parameters {tuple(lead)}")
@@ -176,7 +187,8 @@ class BFGSSolver(Module):
             fn.visibility.reshape(-1, fn.num_views, fn.num_points), fn.num_views, fn.num_points, fn.distortion,
             sufficient_decrease=self.sufficient_decrease, curvature=self.curvature,
             error_threshold=error_threshold, iterations=num_iterations, minimum_step=self.minimum_step,
-            hessian_mode=mode, want_status=True, residual=fn.residual, drop_path_p=drop_p, drop_seed=seed)
+            hessian_mode=mode, want_status=True, residual=fn.residual, drop_path_p=drop_p, drop_seed=seed,
+            return_second_last=second_last)
         self.last_status = status
         return x.reshape(parameters.shape)
 

@@ -71,9 +71,12 @@ def ba_solve(x0: torch.Tensor, observations: torch.Tensor, visibility: torch.Ten
              error_threshold: float = 1e-4, iterations: int = 1000, minimum_step: float = 1e-8,
              max_line_search_trials: int = 1000, strong: bool = True, hessian_mode: int = N.DAVA_HESSIAN_DENSE,
              want_error: bool = False, want_status: bool = False, workspace: Optional[torch.Tensor] = None,
-             residual: int = N.DAVA_RESIDUAL_SQUARED_REPROJECTION, drop_path_p: float = 0.0, drop_seed: int = 0):
+             residual: int = N.DAVA_RESIDUAL_SQUARED_REPROJECTION, drop_path_p: float = 0.0, drop_seed: int = 0,
+             return_second_last: bool = False):
     """One fused launch for the whole batch (``torch.ops.dava.ba_solve``).  Returns (x, error|None, status|None).
-    ``drop_path_p`` > 0: training mode's drop path with the counter-based schedule of ``drop_seed``."""
+    ``drop_path_p`` > 0: training mode's drop path with the counter-based schedule of ``drop_seed``.
+    ``return_second_last``: a problem stopped by the minimum-step rule returns x before its last step
+    (see :func:`second_last_moves_rows` for the one case the reference does differently)."""
     x0 = _fp32_on_device(x0, "parameters")
     obs, vis = _scene_inputs(x0, observations, visibility)
     x, err, status = torch.ops.dava.ba_solve(
@@ -81,8 +84,28 @@ def ba_solve(x0: torch.Tensor, observations: torch.Tensor, visibility: torch.Ten
         float(curvature), float(error_threshold), int(iterations), float(minimum_step), int(max_line_search_trials),
         bool(strong), int(hessian_mode), int(residual), bool(want_error),
         workspace if workspace is not None else x0.new_empty((0,), dtype=torch.uint8), float(drop_path_p),
-        int(drop_seed))
+        int(drop_seed), bool(return_second_last))
     return x, (err if want_error else None), (status if want_status else None)
+
+
+def second_last_moves_rows(status: torch.Tensor) -> bool:
+    """Would the reference's return_second_last scatter (bfgs_solver.py:196-212) have moved rows between
+    problems in this solve?  At iteration k it scatters the step-updated rows of the problems that were
+    active in the line search into the problems still active after the minimum-step test, in batch
+    order: row i of the first set lands on the i-th problem of the second.  That is the identity exactly
+    when every problem stopping by the minimum-step rule at k comes after every problem passing it at k.
+    From the status words: a problem that stopped by the rule (DAVA_STOP_STEP) after s steps failed it at
+    iteration s - 1; any other problem passed it at iterations 0 .. s - 1 (s - 2 for the rule's own).
+    One host sync."""
+    st = status.reshape(-1, N.STATUS_WORDS)
+    if st.shape[0] < 2:
+        return False
+    steps, by_rule = st[:, 0].long(), st[:, 1] == N.STOP_STEP
+    last_pass = steps - 1 - by_rule.long()  # last iteration at which the problem passed the test
+    # largest last_pass among the problems AFTER each one (suffix maximum, exclusive)
+    after = torch.flip(torch.cummax(torch.flip(last_pass, [0]), 0).values, [0])
+    after = torch.cat([after[1:], after.new_full((1,), -2)])
+    return bool((by_rule & (after >= steps - 1)).any().item())
 
 
 def solve_tape_supported(batch: int, num_views: int, num_points: int, distortion: bool, iterations: int,
@@ -102,13 +125,18 @@ class _FusedSolve(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x0, observations, visibility, num_views, num_points, distortion, residual, cfg):
-        c1, c2, thr, iters, min_step, trials, strong, drop_p, drop_seed = cfg
+        c1, c2, thr, iters, min_step, trials, strong, drop_p, drop_seed, second_last = cfg
         x0c = _fp32_on_device(x0, "parameters")
         obs, vis = _scene_inputs(x0c, observations, visibility)
         x, status, tape = torch.ops.dava.ba_solve_record(
             x0c, obs, vis, int(num_views), int(num_points), bool(distortion), float(c1), float(c2), float(thr),
-            int(iters), float(min_step), int(trials), bool(strong), int(residual), float(drop_p), int(drop_seed))
-        ctx.save_for_backward(tape, status, obs, vis)
+            int(iters), float(min_step), int(trials), bool(strong), int(residual), float(drop_p), int(drop_seed),
+            bool(second_last))
+        replay = status
+        if second_last:  # a minimum-step stop returned x before its last step: the adjoint replays one fewer
+            replay = status.clone()
+            replay[:, 0] -= (status[:, 1] == N.STOP_STEP).to(torch.int32)
+        ctx.save_for_backward(tape, replay, obs, vis)
         ctx.meta = (int(num_views), int(num_points), bool(distortion), int(iters), int(residual))
         ctx.mark_non_differentiable(status)
         ctx.recorded = torch.cuda.Event()  # the tape is complete once the recording launch is
@@ -136,11 +164,11 @@ def ba_solve_differentiable(x0: torch.Tensor, observations: torch.Tensor, visibi
                             curvature: float = 0.9, error_threshold: float = 1e-4, iterations: int = 1000,
                             minimum_step: float = 1e-8, max_line_search_trials: int = 1000, strong: bool = True,
                             residual: int = N.DAVA_RESIDUAL_SQUARED_REPROJECTION, drop_path_p: float = 0.0,
-                            drop_seed: int = 0):
+                            drop_seed: int = 0, return_second_last: bool = False):
     """The fused COMPACT solve as an autograd node w.r.t. x0 and the observations.
     Returns (x, status)."""
     cfg = (sufficient_decrease, curvature, error_threshold, iterations, minimum_step, max_line_search_trials, strong,
-           drop_path_p, drop_seed)
+           drop_path_p, drop_seed, return_second_last)
     return _FusedSolve.apply(x0, observations, visibility, num_views, num_points, distortion, residual, cfg)
 
 

@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define DAVA_ABI_VERSION 3
+#define DAVA_ABI_VERSION 4
 
 enum DavaStatus {
   DAVA_OK = 0,
@@ -101,6 +101,13 @@ typedef struct DavaSolverConfig {
    * same schedule on any launch shape.  0 = eval mode (the default).                           */
   float drop_path_p;
   uint32_t drop_seed_lo, drop_seed_hi;
+  /* Training mode's return_second_last (bfgs_solver.py:196-212): a problem that stops by the
+   * minimum-step rule returns the parameters BEFORE its last step (x_k, not x_{k+1}); every other
+   * stop returns the current ones, as without it.  0 = off (the default).  The reference's own
+   * masked_scatter also moves rows between problems when a problem stops this way while a later
+   * problem of the batch continues; the caller detects that case from the status words (the Python
+   * module then runs the reference's loop instead).                                */
+  int32_t return_second_last;
 } DavaSolverConfig;
 
 /* Per-problem status written by dava_ba_solve: int32 (B, 4) =

@@ -459,3 +459,93 @@ def test_fused_adjoint_through_a_training_mode_solve(device):
         assert _rows_rel(xd.grad.cpu()[idx], gx_ref).max() <= 2e-3, (steps, idx.tolist(),
                                                                       _rows_rel(xd.grad.cpu()[idx], gx_ref).tolist())
         assert _rows_rel(od.grad.cpu()[idx], go_ref).max() <= 2e-3, steps
+
+
+# ---- global-vector mode (P > 1024 or an image past the CU's LDS, e.g. C5): the adjoint's O(P)
+# vectors live in its workspace and its passes run workgroup-wide (csrc/bfgs_adjoint.hip, GT > 0) ----
+
+@pytest.mark.parametrize("ray", [False, True])
+def test_gv_adjoint_matches_lds_adjoint(device, ray, monkeypatch):
+    """One C3-shaped tape replayed by both adjoint kernels (DAVA_ADJ_FORCE_GV): the same math with
+    the vectors in HBM and a different summation order -- gradients agree to fp32 reordering."""
+    from deep_attention_visual_odometry_amd import make_scenes
+
+    m, n, k, dist = 4, 256, 24, not ray
+    s = make_scenes(8, m, n, distortion=dist, seed=936, drop=0.0, ray_angle=ray)
+    x0, obs, vis = (torch.tensor(t).to(device) for t in (s.initial, s.observations, s.visibility))
+    vis = vis.to(torch.uint8)
+    res = 1 if ray else 0
+    w = torch.randn(x0.shape, generator=torch.Generator().manual_seed(6)).to(device)
+    x, status, tape = torch.ops.dava.ba_solve_record(x0, obs, vis, m, n, dist, 1e-4, 0.9, -1.0, k, -1.0, 1000, True,
+                                                     res)
+    assert (status[:, 0] == k).all() and torch.isfinite(x).all()
+    gx, gobs = torch.ops.dava.ba_solve_backward(w, tape, status, obs, vis, m, n, dist, k, res, True)
+    monkeypatch.setenv("DAVA_ADJ_FORCE_GV", "1")
+    gx_gv, gobs_gv = torch.ops.dava.ba_solve_backward(w, tape, status, obs, vis, m, n, dist, k, res, True)
+    rx, ro = _rows_rel(gx_gv.cpu(), gx.cpu()), _rows_rel(gobs_gv.cpu(), gobs.cpu())
+    print("GV vs LDS adjoint", "ray" if ray else "sq", rx.max().item(), ro.max().item())
+    # the ray angle's second derivatives grow like 1 / |residual| as residuals vanish, so reduction order
+    # moves its gradients ~100x more than the squared objective's (test_fused_adjoint_matches_oracle)
+    tol = 2e-3 if ray else 1e-4
+    assert rx.max() <= tol and ro.max() <= tol, (rx, ro)
+
+
+def test_gv_recording_is_bitwise_the_gv_solve(device, monkeypatch):
+    """A global-vector-mode recording (DAVA_FORCE_GV at the C3 shape: the forward's vectors in the
+    tape's own region, wide history pass writing the tape rows) returns exactly the GV solve's x and
+    status."""
+    from deep_attention_visual_odometry_amd import make_scenes, native_ops
+
+    monkeypatch.setenv("DAVA_FORCE_GV", "1")
+    s = make_scenes(16, 4, 256, distortion=True, seed=937, drop=0.0)
+    x0, obs, vis = (torch.tensor(t).to(device) for t in (s.initial, s.observations, s.visibility))
+    kw = dict(iterations=30, error_threshold=-1.0, minimum_step=-1.0)
+    x, _, st = native_ops.ba_solve(x0, obs, vis, 4, 256, True, hessian_mode=1, want_status=True, **kw)
+    xr, str_ = native_ops.ba_solve_differentiable(x0, obs, vis, 4, 256, True, **kw)
+    assert torch.equal(x, xr) and torch.equal(st, str_)
+
+
+@pytest.mark.parametrize("m,n,distortion,force_gv,k,b", [
+    (4, 256, True, True, 8, 2),     # GV forward (forced) + GV adjoint, Brown-Conrady
+    (4, 400, False, False, 10, 2),  # P = 1221 > 1024: LDS-mode forward, GV adjoint
+    (3, 1300, True, False, 6, 1),   # P = 3920: GV forward (wide pass, GT = 2), ragged points per thread
+])
+def test_gv_adjoint_matches_oracle(device, m, n, distortion, force_gv, k, b, monkeypatch):
+    """d (w . x_K) / d x0 and / d obs through a solve whose adjoint runs in global-vector mode, vs
+    autograd through the oracle's fp32 restatement of the reference's loop (create_graph)."""
+    from deep_attention_visual_odometry_amd import make_scenes
+
+    if force_gv:
+        monkeypatch.setenv("DAVA_FORCE_GV", "1")
+        monkeypatch.setenv("DAVA_ADJ_FORCE_GV", "1")
+    s = make_scenes(b, m, n, distortion=distortion, seed=950 + n + k, drop=0.0 if distortion else 0.1)
+    x0, obs, vis = torch.tensor(s.initial), torch.tensor(s.observations), torch.tensor(s.visibility)
+    w = torch.randn(x0.shape, generator=torch.Generator().manual_seed(k))
+    kw = dict(iterations=k, error_threshold=-1.0, minimum_step=-1.0)
+    out, gx, go, st = _fused_grads(device, x0, obs, vis, m, n, distortion, w, **kw)
+    ref, gx_ref, go_ref = _oracle_grads(x0, obs, vis, m, n, distortion, w, **kw)
+    assert (st[:, 0] == k).all()
+    assert _rows_rel(out, ref).max() <= 1e-5
+    rx, ro = _rows_rel(gx, gx_ref), _rows_rel(go, go_ref)
+    print("GV ADJOINT", m, n, distortion, force_gv, k, "x0", rx.max().item(), "obs", ro.max().item())
+    assert rx.max() <= 2e-3 and ro.max() <= 2e-3, (rx, ro)
+
+
+def test_c5_shape_gradient_through_the_solve(device):
+    """C5 shape (16 views x 4096 points, P = 12381), the configuration the generic loop cannot
+    differentiate at batch scale (a dense 613 MB H per problem per iteration in the graph): the GV
+    recording + adjoint against oracle autograd through K = 3 iterations of one problem."""
+    from deep_attention_visual_odometry_amd import make_scenes, native_ops
+
+    assert native_ops.solve_tape_supported(1, 16, 4096, False, 3)  # the fused path, not the generic loop
+    s = make_scenes(1, 16, 4096, distortion=False, seed=958, drop=0.1)
+    x0, obs, vis = torch.tensor(s.initial), torch.tensor(s.observations), torch.tensor(s.visibility)
+    w = torch.randn(x0.shape, generator=torch.Generator().manual_seed(9))
+    kw = dict(iterations=3, error_threshold=-1.0, minimum_step=-1.0)
+    out, gx, go, st = _fused_grads(device, x0, obs, vis, 16, 4096, False, w, **kw)
+    ref, gx_ref, go_ref = _oracle_grads(x0, obs, vis, 16, 4096, False, w, **kw)
+    assert (st[:, 0] == 3).all()
+    assert _rows_rel(out, ref).max() <= 1e-5
+    rx, ro = _rows_rel(gx, gx_ref), _rows_rel(go, go_ref)
+    print("C5 ADJOINT x0", rx.max().item(), "obs", ro.max().item())
+    assert rx.max() <= 2e-3 and ro.max() <= 2e-3, (rx, ro)

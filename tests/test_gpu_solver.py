@@ -638,12 +638,12 @@ def test_fused_drop_path_is_the_eval_solve_stopped_early(device):
 
 
 def test_infeasible_generic_fallback_raises(device):
-    """Differentiating a GV-mode (C5-shaped) solve has no fused adjoint; the generic loop would hold
-    the dense (B, P, P) inverse Hessian per iteration in the graph (hundreds of GiB): refused up
-    front with a RuntimeError, never attempted."""
+    """Differentiating a solve past the fused adjoint's reach (P = 15093 > 14336: more than 14 float4
+    groups per thread) falls to the generic loop, which would hold the dense (B, P, P) inverse Hessian
+    per iteration in the graph (hundreds of GiB): refused up front with a RuntimeError, never attempted."""
     from deep_attention_visual_odometry_amd import BFGSSolver, ReprojectionError
 
-    m, n = 16, 4096
+    m, n = 16, 5000
     p = 3 + 3 * n + 6 * (m - 1)
     fn = ReprojectionError(torch.zeros(2, m, n, 2, device=device), torch.ones(2, m, n, device=device), m, n)
     x0 = torch.zeros(2, p, device=device, requires_grad=True)
@@ -674,3 +674,111 @@ def test_reference_defaults_c2_objective_parity(device):
              "steps_ref_mean": float(rec.iterations.double().mean())})
     assert (status[:, 1] != 0).all()  # stopped by a rule, not the cap
     assert (e_gpu <= 1.05 * torch.clamp(e_ref, min=1e-4)).all(), (e_gpu, e_ref)
+
+
+# ---- training mode's return_second_last, fused (bfgs_solver.py:196-212) ----
+
+def _second_last_case(device, b=32, seed=581, min_step=2e-3):
+    x0, obs, vis = _scene(b, 2, 64, False, seed)
+    kw = dict(iterations=60, error_threshold=-1.0, minimum_step=min_step)
+    return x0, obs, vis, kw
+
+
+def test_fused_second_last_is_the_solve_before_its_last_step(device):
+    """return_second_last in the fused kernel: a problem stopped by the minimum-step rule returns
+    exactly the eval solve run for one step fewer (x before the step that failed the test); every
+    other problem returns exactly what it returns without the flag."""
+    from deep_attention_visual_odometry_amd import native_ops
+
+    x0, obs, vis, kw = _second_last_case(device)
+    args = (x0.to(device), obs.to(device), vis.to(device), 2, 64, False)
+    plain, _, st = native_ops.ba_solve(*args, hessian_mode=1, want_status=True, **kw)
+    sl, _, st_sl = native_ops.ba_solve(*args, hessian_mode=1, want_status=True, return_second_last=True, **kw)
+    plain, sl, st, st_sl = plain.cpu(), sl.cpu(), st.cpu(), st_sl.cpu()
+    assert torch.equal(st, st_sl)
+    by_rule = st[:, 1] == 2  # DAVA_STOP_STEP
+    assert by_rule.sum() >= 4 and (~by_rule).sum() >= 1
+    assert torch.equal(sl[~by_rule], plain[~by_rule])
+    for steps in st[by_rule, 0].unique().tolist():
+        idx = (by_rule & (st[:, 0] == steps)).nonzero().flatten()
+        ref, _, _ = native_ops.ba_solve(x0[idx].to(device), obs[idx].to(device), vis[idx].to(device), 2, 64, False,
+                                        iterations=int(steps) - 1, error_threshold=-1.0, minimum_step=-1.0,
+                                        hessian_mode=1)
+        assert torch.equal(sl[idx], ref.cpu()), steps
+
+
+def test_fused_second_last_matches_oracle(device):
+    """BFGSSolver(return_second_last=True) in training mode (drop path off) against the oracle's
+    training-mode loop, which includes the reference's row-moving scatter.  Batches of one problem
+    (no scatter can move a row) run fused; a batch where the scatter moves rows is redone by the
+    generic loop -- either way the result is the reference's."""
+    from deep_attention_visual_odometry_amd import BFGSSolver, ReprojectionError, native_ops
+
+    x0, obs, vis, kw = _second_last_case(device, b=12)
+    solver_kw = dict(drop_path_p=0.0, return_second_last=True, training_iterations=kw["iterations"],
+                     training_error_threshold=kw["error_threshold"], minimum_step=kw["minimum_step"])
+    fn_ref = objective.ReprojectionClosure(obs, vis, 2, 64)
+    ref = solver.bfgs_solve(x0, fn_ref, training=True, return_second_last=True, drop_path_p=0.0, **kw)
+    s = BFGSSolver(**solver_kw)
+    out = s(x0.to(device), ReprojectionError(obs.to(device), vis.to(device), 2, 64)).cpu()
+    rel = _rel(out, ref)
+    assert (rel <= TOL).all(), rel
+    # one problem at a time: always the fused kernel (a single problem cannot move rows)
+    for i in range(4):
+        si = BFGSSolver(**solver_kw)
+        oi = si(x0[i:i + 1].to(device), ReprojectionError(obs[i:i + 1].to(device), vis[i:i + 1].to(device), 2, 64))
+        assert si.last_status is not None  # the fused path ran
+        ri = solver.bfgs_solve(x0[i:i + 1], objective.ReprojectionClosure(obs[i:i + 1], vis[i:i + 1], 2, 64),
+                               training=True, return_second_last=True, drop_path_p=0.0, **kw)
+        assert _rel(oi.cpu(), ri).max() <= TOL
+
+
+def test_second_last_row_move_falls_back_to_the_reference_loop(device):
+    """A batch whose reference scatter moves rows (a problem stops by the minimum-step rule while a
+    later one continues): the module returns the generic loop's result bit for bit."""
+    from deep_attention_visual_odometry_amd import BFGSSolver, ReprojectionError, native_ops
+
+    x0, obs, vis, kw = _second_last_case(device, b=12)
+    _, _, st = native_ops.ba_solve(x0.to(device), obs.to(device), vis.to(device), 2, 64, False, hessian_mode=1,
+                                   want_status=True, return_second_last=True, **kw)
+    assert native_ops.second_last_moves_rows(st)
+    solver_kw = dict(drop_path_p=0.0, return_second_last=True, training_iterations=kw["iterations"],
+                     training_error_threshold=kw["error_threshold"], minimum_step=kw["minimum_step"])
+    fn = ReprojectionError(obs.to(device), vis.to(device), 2, 64)
+    s = BFGSSolver(**solver_kw)
+    out = s(x0.to(device), fn)
+    assert s.last_status is None  # the generic loop ran
+    g = BFGSSolver(**solver_kw)
+    ref = g._generic(x0.to(device), fn, kw["error_threshold"], kw["iterations"])
+    assert torch.equal(out, ref)
+
+
+def test_fused_second_last_gradient_matches_oracle(device):
+    """Differentiating a training-mode return_second_last solve of one problem that stops by the
+    minimum-step rule: the adjoint replays one step fewer, matching oracle autograd."""
+    from deep_attention_visual_odometry_amd import BFGSSolver, ReprojectionError
+
+    x0, obs, vis, kw = _second_last_case(device, b=8)
+    w = torch.randn(x0.shape, generator=torch.Generator().manual_seed(12))
+    solver_kw = dict(drop_path_p=0.0, return_second_last=True, training_iterations=kw["iterations"],
+                     training_error_threshold=kw["error_threshold"], minimum_step=kw["minimum_step"])
+    checked = 0
+    for i in range(8):
+        xd = x0[i:i + 1].to(device).requires_grad_(True)
+        od = obs[i:i + 1].to(device).requires_grad_(True)
+        s = BFGSSolver(**solver_kw)
+        out = s(xd, ReprojectionError(od, vis[i:i + 1].to(device), 2, 64))
+        if int(s.last_status[0, 1]) != 2:
+            continue
+        (out * w[i:i + 1].to(device)).sum().backward()
+        xr = x0[i:i + 1].clone().requires_grad_(True)
+        orr = obs[i:i + 1].clone().requires_grad_(True)
+        ref = solver.bfgs_solve(xr, objective.ReprojectionClosure(orr, vis[i:i + 1], 2, 64), training=True,
+                                return_second_last=True, drop_path_p=0.0, **kw)
+        (ref * w[i:i + 1]).sum().backward()
+        assert _rel(out.detach().cpu(), ref.detach()).max() <= TOL
+        gx = ((xd.grad.cpu() - xr.grad).norm() / xr.grad.norm()).item()
+        go = ((od.grad.cpu() - orr.grad).norm() / orr.grad.norm()).item()
+        assert gx <= 2e-3 and go <= 2e-3, (i, gx, go)
+        checked += 1
+    assert checked >= 2

@@ -45,7 +45,7 @@ def test_python_binding_types_every_declared_symbol():
 
 def test_library_is_built_for_gfx950(lib):
     assert lib.dava_device_arch() == b"gfx950"
-    assert lib.dava_abi_version() == 3
+    assert lib.dava_abi_version() == 4
     blob = open(lib._name, "rb").read()
     assert b"gfx950" in blob
 
@@ -105,6 +105,29 @@ def test_solve_plan(lib, monkeypatch):
     monkeypatch.setenv("DAVA_LDS_HISTORY", "1000")  # clamped to one workgroup's LDS
     big = native_ops.solve_plan(8192, 4, 256, True, 1, 100)
     assert big["lds_bytes"] <= 160 * 1024 and big["lds_history_entries"] > c3["lds_history_entries"]
+
+
+def test_adjoint_shapes(lib):
+    """Host-only: which shapes have the fused adjoint.  C3 (P = 794) runs it with the O(P) vectors in
+    LDS; C5 (P = 12381, the forward's global-vector mode) with them in the adjoint's workspace, and its
+    tape holds the forward's vector slices too; past P = 14336 (14 float4 groups per thread) there is
+    none, and the dense mode never records."""
+    from deep_attention_visual_odometry_amd import _native as N, native_ops
+
+    assert native_ops.solve_tape_supported(8192, 4, 256, True, 100)
+    assert native_ops.solve_tape_supported(256, 16, 4096, False, 100)
+    assert not native_ops.solve_tape_supported(2, 16, 5000, False, 100)  # P = 15093
+    sc = native_ops.scene_struct(None, None, 16, 4096, False, 256, N.DAVA_RESIDUAL_SQUARED_REPROJECTION)
+    cfg = native_ops.solver_config(1e-4, 0.9, -1.0, 100, -1.0, 1000, True, N.DAVA_HESSIAN_COMPACT)
+    p, pv, k = 12381, 12384, 100
+    t = (3 * k + 1 + 3) // 4 * 4
+    floats = 256 * (2 * (k - 1) * pv + 2 * k * pv + t + 9 * pv)  # history, x, g, scalars, GV vectors
+    assert lib.dava_ba_solve_tape_bytes(sc, cfg) == floats * 4 + 256
+    # adjoint workspace: the a rows (B, K, Pv) plus 18 Pv floats of vectors per problem
+    assert lib.dava_ba_solve_backward_workspace_bytes(sc, cfg) == 256 * (k + 18) * pv * 4 + 256
+    assert lib.dava_ba_solve_backward_lds_entries(sc, cfg) == 0
+    cfg_dense = native_ops.solver_config(1e-4, 0.9, -1.0, 100, -1.0, 1000, True, N.DAVA_HESSIAN_DENSE)
+    assert lib.dava_ba_solve_tape_bytes(sc, cfg_dense) == 0
 
 
 def test_product_refuses_cpu_tensors():
