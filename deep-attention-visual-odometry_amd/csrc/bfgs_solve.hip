@@ -158,6 +158,27 @@ __device__ __forceinline__ f4v pk_fma4(float k, f4v v, f4v c) {
 __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
 __device__ __forceinline__ void st4(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
 
+// Buffer loads (SRD in SGPRs, 32-bit per-lane byte offset): no 64-bit address arithmetic per
+// load, and the descriptor's range check returns zeros past `bytes` with no branch.
+__device__ __forceinline__ const float* uniform_ptr(const float* p) {
+  const unsigned long long v = reinterpret_cast<unsigned long long>(p);
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v);
+  const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
+  return reinterpret_cast<const float*>(((unsigned long long)hi << 32) | lo);
+}
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const float* p, int bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p), (short)0, bytes, 0x00020000);
+}
+__device__ __forceinline__ f4v buf_ld4(__amdgpu_buffer_rsrc_t r, int voff) {
+  return __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(r, voff, 0, 0));
+}
+#ifndef DAVA_GV_BUFFER_LOADS
+#define DAVA_GV_BUFFER_LOADS 0  // 1: GV wide pass rows through buffer loads (bitwise equal; C5 -1.8 .. +2.5%, not enabled)
+#endif
+#ifndef DAVA_FUSED_BUFFER_LOADS
+#define DAVA_FUSED_BUFFER_LOADS 0  // 1: LDS-mode fused pass rows through buffer loads (bitwise equal; C2 +1-3%, C3 -6%)
+#endif
+
 #ifndef DAVA_SWEEP_ROWS
 #define DAVA_SWEEP_ROWS 4
 #endif
@@ -582,7 +603,88 @@ __device__ __forceinline__ float wide_direction(int P, int Pv, int nh, const flo
       }
     }
   }
+#if DAVA_GV_BUFFER_LOADS
+  if constexpr (!HYD) {
+    // Rows through buffer loads: one descriptor per row with the row's length as its range, so the
+    // absent column groups past P load zeros with no exec-mask branch, and each load's address is a
+    // loop-invariant 32-bit lane offset instead of 64-bit arithmetic per load and entry (~100 fewer
+    // instructions per entry and wave at C5).  Same values, same order as the plain loop below:
+    // bitwise equal, but not a reliable gain: interleaved A/B on three boxes, C5 -1.8% on one and
+    // +2.5% on two (profiles/r03_ab_buffer_loads.log) -- the GV kernel's register allocation (at
+    // the 256-VGPR cap, ~90 spilled) moves with any change.  Rejected outright: requesting the next
+    // entry's rows before this entry's reduction (all of them, or the S row only) -- the second set
+    // of rows spills inside the loop, C5 -40..-45%.
+    const float* Su = uniform_ptr(S);
+    const float* Wu = uniform_ptr(W);
+    const int row_bytes = 4 * Pv;
+    int voff[GT];
+#pragma unroll
+    for (int u = 0; u < GT; ++u) voff[u] = 16 * (tid + u * BLOCK);
+    auto load_group = [&](int j, f4v (&s4)[E][GT], f4v (&w4)[E][GT]) {
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        const int nb = j + e < nh ? row_bytes : 0;  // uniform: an absent entry reads zeros
+        const auto rs = make_rsrc(Su + (size_t)(j + e) * Pv, nb);
+        const auto rw = make_rsrc(Wu + (size_t)(j + e) * Pv, nb);
+#pragma unroll
+        for (int u = 0; u < GT; ++u) {
+          s4[e][u] = buf_ld4(rs, voff[u]);
+          w4[e][u] = buf_ld4(rw, voff[u]);
+        }
+      }
+    };
+    auto dots = [&](const f4v (&s4)[E][GT], const f4v (&w4)[E][GT], float (&dd)[4 * E]) {
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        f2v sy2 = {0.f, 0.f}, wy2 = {0.f, 0.f}, sg2 = {0.f, 0.f}, wg2 = {0.f, 0.f};
+#pragma unroll
+        for (int u = 0; u < GT; ++u) {
+          sy2 = pk_fma(s4[e][u].lo, y[u].lo, sy2); sy2 = pk_fma(s4[e][u].hi, y[u].hi, sy2);
+          wy2 = pk_fma(w4[e][u].lo, y[u].lo, wy2); wy2 = pk_fma(w4[e][u].hi, y[u].hi, wy2);
+          sg2 = pk_fma(s4[e][u].lo, gg[u].lo, sg2); sg2 = pk_fma(s4[e][u].hi, gg[u].hi, sg2);
+          wg2 = pk_fma(w4[e][u].lo, gg[u].lo, wg2); wg2 = pk_fma(w4[e][u].hi, gg[u].hi, wg2);
+        }
+        dd[4 * e] = sy2.x + sy2.y;
+        dd[4 * e + 1] = wy2.x + wy2.y;
+        dd[4 * e + 2] = sg2.x + sg2.y;
+        dd[4 * e + 3] = wg2.x + wg2.y;
+      }
+    };
+    auto accumulate = [&](int j, const f4v (&s4)[E][GT], const f4v (&w4)[E][GT], const float (&dd)[4 * E],
+                          const float (&rh)[E], const float (&ch)[E]) {
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        if (j + e < nh) {
+          const float rho = rh[e], cr = ch[e] * rho;
+          const float ay = fmaf(cr, dd[4 * e], -(rho * dd[4 * e + 1])), by = -rho * dd[4 * e];
+          const float ag = fmaf(cr, dd[4 * e + 2], -(rho * dd[4 * e + 3])), bg = -rho * dd[4 * e + 2];
+#pragma unroll
+          for (int u = 0; u < GT; ++u) {
+            pa[u] = pk_fma4(by, w4[e][u], pk_fma4(ay, s4[e][u], pa[u]));
+            pb[u] = pk_fma4(bg, w4[e][u], pk_fma4(ag, s4[e][u], pb[u]));
+          }
+        }
+      }
+    };
+    for (int j = 0; j < nh; j += E) {
+      f4v sA[E][GT], wA[E][GT];
+      float dd[4 * E], rh[E], ch[E];
+      load_group(j, sA, wA);
+      dots(sA, wA, dd);
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        rh[e] = hrho[min(j + e, nh - 1)];
+        ch[e] = hc[min(j + e, nh - 1)];
+      }
+      block_sum<4 * E, NW>(dd, scratch, buf);
+      buf ^= 1;
+      accumulate(j, sA, wA, dd, rh, ch);
+    }
+  }
+  for (int j = 0; j < 0; j += E) {
+#else
   for (int j = 0; j < (HYD ? 0 : nh); j += E) {
+#endif
     const int ne = min(E, nh - j);  // uniform
     f4v s4[E][GT], w4[E][GT];
     float dd[4 * E];
@@ -831,6 +933,21 @@ __device__ __forceinline__ void compact_products_fused(int P, int Pv, int nh, co
 #endif
     }
   };
+#if DAVA_FUSED_BUFFER_LOADS
+  // buffer loads: a descriptor per row (range = the row), lane offsets loop-invariant, the groups
+  // past P read zeros through the range check instead of an exec-mask branch (bitwise equal)
+  const float* Su = uniform_ptr(S);
+  const float* Wu = uniform_ptr(W);
+  auto load = [&](int j, f4v (&s4)[GM], f4v (&w4)[GM]) {
+    const auto rs = make_rsrc(Su + (size_t)j * Pv, 4 * Pv);
+    const auto rw = make_rsrc(Wu + (size_t)j * Pv, 4 * Pv);
+#pragma unroll
+    for (int m = 0; m < GM; ++m) {
+      s4[m] = buf_ld4(rs, 16 * (lane + kWave * m));
+      w4[m] = buf_ld4(rw, 16 * (lane + kWave * m));
+    }
+  };
+#else
   auto load = [&](int j, f4v (&s4)[GM], f4v (&w4)[GM]) {
     const float* sr = S + (size_t)j * Pv;
     const float* wr = W + (size_t)j * Pv;
@@ -841,6 +958,7 @@ __device__ __forceinline__ void compact_products_fused(int P, int Pv, int nh, co
       w4[m] = ok[m] ? *reinterpret_cast<const f4v*>(wr + 4 * q) : f4v{0, 0, 0, 0};
     }
   };
+#endif
 #if DAVA_HIST_PRIO != DAVA_BASE_PRIO
   __builtin_amdgcn_s_setprio(DAVA_HIST_PRIO);
 #endif

@@ -692,6 +692,10 @@ def test_fused_second_last_is_the_solve_before_its_last_step(device):
 
     x0, obs, vis, kw = _second_last_case(device)
     args = (x0.to(device), obs.to(device), vis.to(device), 2, 64, False)
+    # cap the iterations at the median stopping step, so that the batch holds problems stopped by
+    # the minimum-step rule and problems stopped by the cap
+    _, _, st0 = native_ops.ba_solve(*args, hessian_mode=1, want_status=True, **kw)
+    kw = dict(kw, iterations=max(2, int(st0[:, 0].float().median().item())))
     plain, _, st = native_ops.ba_solve(*args, hessian_mode=1, want_status=True, **kw)
     sl, _, st_sl = native_ops.ba_solve(*args, hessian_mode=1, want_status=True, return_second_last=True, **kw)
     plain, sl, st, st_sl = plain.cpu(), sl.cpu(), st.cpu(), st_sl.cpu()
@@ -711,18 +715,36 @@ def test_fused_second_last_matches_oracle(device):
     """BFGSSolver(return_second_last=True) in training mode (drop path off) against the oracle's
     training-mode loop, which includes the reference's row-moving scatter.  Batches of one problem
     (no scatter can move a row) run fused; a batch where the scatter moves rows is redone by the
-    generic loop -- either way the result is the reference's."""
+    generic loop -- either way the result is the reference's.
+
+    In the batch, the scatter hands most problems another problem's parameters from iteration 1 on
+    (problem 1 stops first, so row i lands on problem i + 1), and those problems then solve from a
+    foreign start: the reference itself moves 3 of the 12 results by ~0.4 under a 1-ulp nudge of x0.
+    So the batch is held per problem to max(1e-5, 10x the oracle's 1-ulp spread), and a problem the
+    oracle leaves at the iteration cap (not converged: a wandering trajectory whose 1-ulp spread
+    under-samples its sensitivity) only has to be finite; the module's result is also bitwise the
+    generic loop's (test_second_last_row_move_falls_back_to_the_reference_loop), whose scatter is
+    pinned to the reference's own output (tests/golden/training.npz)."""
     from deep_attention_visual_odometry_amd import BFGSSolver, ReprojectionError, native_ops
 
     x0, obs, vis, kw = _second_last_case(device, b=12)
     solver_kw = dict(drop_path_p=0.0, return_second_last=True, training_iterations=kw["iterations"],
                      training_error_threshold=kw["error_threshold"], minimum_step=kw["minimum_step"])
     fn_ref = objective.ReprojectionClosure(obs, vis, 2, 64)
-    ref = solver.bfgs_solve(x0, fn_ref, training=True, return_second_last=True, drop_path_p=0.0, **kw)
+    rec = solver.SolveRecord(torch.empty(0), torch.empty(0))
+    ref = solver.bfgs_solve(x0, fn_ref, training=True, return_second_last=True, drop_path_p=0.0, record=rec, **kw)
+    env = torch.zeros(x0.shape[0], dtype=torch.float64)
+    for sgn in (1.0, -1.0):
+        xn = torch.nextafter(x0, x0 + sgn * float("inf"))
+        env = torch.maximum(env, _rel(solver.bfgs_solve(xn, fn_ref, training=True, return_second_last=True,
+                                                        drop_path_p=0.0, **kw), ref))
     s = BFGSSolver(**solver_kw)
     out = s(x0.to(device), ReprojectionError(obs.to(device), vis.to(device), 2, 64)).cpu()
     rel = _rel(out, ref)
-    assert (rel <= TOL).all(), rel
+    capped = rec.reason == solver.STOP_ITERATIONS
+    assert int((~capped).sum()) >= 8
+    assert torch.isfinite(out).all()
+    assert ((rel <= torch.clamp(10.0 * env, min=TOL)) | capped).all(), (rel, env, capped)
     # one problem at a time: always the fused kernel (a single problem cannot move rows)
     for i in range(4):
         si = BFGSSolver(**solver_kw)
