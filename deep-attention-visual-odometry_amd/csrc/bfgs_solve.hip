@@ -173,7 +173,7 @@ __device__ __forceinline__ f4v buf_ld4(__amdgpu_buffer_rsrc_t r, int voff) {
   return __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(r, voff, 0, 0));
 }
 #ifndef DAVA_GV_BUFFER_LOADS
-#define DAVA_GV_BUFFER_LOADS 0  // 1: GV wide pass rows through buffer loads (bitwise equal; C5 -1.8 .. +2.5%, not enabled)
+#define DAVA_GV_BUFFER_LOADS 0  // 1: GV wide pass rows through buffer loads (bitwise equal; C5 -2.5 .. +1.8%, not enabled)
 #endif
 #ifndef DAVA_FUSED_BUFFER_LOADS
 #define DAVA_FUSED_BUFFER_LOADS 0  // 1: LDS-mode fused pass rows through buffer loads (bitwise equal; C2 +1-3%, C3 -6%)
@@ -526,6 +526,9 @@ __device__ __forceinline__ void compact_products_wide(int P, int Pv, int nh, con
 #ifndef DAVA_HY_FROM_D
 #define DAVA_HY_FROM_D 0
 #endif
+#ifndef DAVA_HY_FROM_D_LDS
+#define DAVA_HY_FROM_D_LDS 0  // the same for the LDS-mode fused pass (C1-C3)
+#endif
 #ifndef DAVA_GV_ENTRIES_HYD
 #define DAVA_GV_ENTRIES_HYD 2
 #endif
@@ -609,8 +612,8 @@ __device__ __forceinline__ float wide_direction(int P, int Pv, int nh, const flo
     // absent column groups past P load zeros with no exec-mask branch, and each load's address is a
     // loop-invariant 32-bit lane offset instead of 64-bit arithmetic per load and entry (~100 fewer
     // instructions per entry and wave at C5).  Same values, same order as the plain loop below:
-    // bitwise equal, but not a reliable gain: interleaved A/B on three boxes, C5 -1.8% on one and
-    // +2.5% on two (profiles/r03_ab_buffer_loads.log) -- the GV kernel's register allocation (at
+    // bitwise equal, but not a reliable gain: interleaved A/B on three boxes, C5 +1.8% on one and
+    // -2.5% on two (problems/s, profiles/r03_ab_buffer_loads.log) -- the GV kernel's register allocation (at
     // the 256-VGPR cap, ~90 spilled) moves with any change.  Rejected outright: requesting the next
     // entry's rows before this entry's reduction (all of them, or the S row only) -- the second set
     // of rows spills inside the loop, C5 -40..-45%.
@@ -862,9 +865,12 @@ __device__ __forceinline__ void compact_products_fused(int P, int Pv, int nh, co
                                        const float* __restrict__ W, const float* LH, int lcap,
                                        const float* hrho, const float* hc,
                                        float gamma0, const float* g, const float* gp, float* a_out, float* b_out,
-                                       float* spare0, float* spare1, float* spare2, float* spare3) {
+                                       float* spare0, float* spare1, float* spare2, float* spare3,
+                                       const float* dprev) {
   static_assert(NW == 1 || NW == 2 || NW == 4, "the cross-wave combine is written for 1, 2 or 4 waves");
   constexpr int EF = fused_inflight<GM>();
+  constexpr bool HYD = DAVA_HY_FROM_D_LDS;
+  static_assert(!HYD || NW == 1 || DAVA_DEFER_COMBINE, "H'y from d: the deferred cross-wave combine");
   const int lane = threadIdx.x & (kWave - 1);
   const int wave = threadIdx.x / kWave;
   const int G = (P + 3) / 4;
@@ -890,7 +896,43 @@ __device__ __forceinline__ void compact_products_fused(int P, int Pv, int nh, co
   // one transposed wave reduction of the four (wave_sum4: uniform results), then the entry's
   // contribution to H y and H g as packed FMAs.  ~90 VALU ops per entry at GM = 4 (the round-1
   // form, per-element products + one wave_sum per dot: ~210).
+  // HYD (DAVA_HY_FROM_D_LDS): only H'g is formed from the history -- two dots (s.g, w.g) and one
+  // accumulation per entry; H'y = H'g + d_prev after the pass (d_prev = -H' g_prev, the same H').
+  // Two entries share one transposed wave reduction (consume_pair).
+  auto acc_g = [&](int j, float sg, float wg, const f4v (&s4)[GM], const f4v (&w4)[GM]) {
+    const float rho = hrho[j], cr = hc[j] * rho;
+    const float ag = fmaf(cr, sg, -(rho * wg)), bg = -rho * sg;
+#pragma unroll
+    for (int m = 0; m < GM; ++m) pb[m] = pk_fma4(bg, w4[m], pk_fma4(ag, s4[m], pb[m]));
+  };
+  auto gdots = [&](const f4v (&s4)[GM], const f4v (&w4)[GM], float& sg, float& wg) {
+    f2v sg2 = {0.f, 0.f}, wg2 = {0.f, 0.f};
+#pragma unroll
+    for (int m = 0; m < GM; ++m) {
+      const f4v gm = gvec(m);
+      sg2 = pk_fma(s4[m].lo, gm.lo, sg2); sg2 = pk_fma(s4[m].hi, gm.hi, sg2);
+      wg2 = pk_fma(w4[m].lo, gm.lo, wg2); wg2 = pk_fma(w4[m].hi, gm.hi, wg2);
+    }
+    sg = sg2.x + sg2.y;
+    wg = wg2.x + wg2.y;
+  };
+  auto consume_pair = [&](int j0, const f4v (&s0)[GM], const f4v (&w0)[GM], int j1, const f4v (&s1)[GM],
+                          const f4v (&w1)[GM]) {
+    float a0, b0, a1, b1;
+    gdots(s0, w0, a0, b0);
+    gdots(s1, w1, a1, b1);
+    const float4 t = wave_sum4(a0, b0, a1, b1);
+    acc_g(j0, t.x, t.y, s0, w0);
+    acc_g(j1, t.z, t.w, s1, w1);
+  };
   auto consume = [&](int j, const f4v (&s4)[GM], const f4v (&w4)[GM]) {
+    if constexpr (HYD) {
+      float a0, b0;
+      gdots(s4, w4, a0, b0);
+      const float4 t = wave_sum4(a0, b0, 0.f, 0.f);
+      acc_g(j, t.x, t.y, s4, w4);
+      return;
+    }
 #if DAVA_PACKED_HISTORY
     f2v sy2 = {0.f, 0.f}, wy2 = {0.f, 0.f}, sg2 = {0.f, 0.f}, wg2 = {0.f, 0.f};
 #pragma unroll
@@ -1000,8 +1042,13 @@ __device__ __forceinline__ void compact_products_fused(int P, int Pv, int nh, co
       f4v s[EF][GM], w[EF][GM];
 #pragma unroll
       for (int e = 0; e < EF; ++e) load(j + e * NW, s[e], w[e]);
+      if constexpr (HYD && EF % 2 == 0) {
 #pragma unroll
-      for (int e = 0; e < EF; ++e) consume(j + e * NW, s[e], w[e]);
+        for (int e = 0; e < EF; e += 2) consume_pair(j + e * NW, s[e], w[e], j + (e + 1) * NW, s[e + 1], w[e + 1]);
+      } else {
+#pragma unroll
+        for (int e = 0; e < EF; ++e) consume(j + e * NW, s[e], w[e]);
+      }
     }
 #endif
   }
@@ -1037,13 +1084,42 @@ __device__ __forceinline__ void compact_products_fused(int P, int Pv, int nh, co
 #pragma unroll
     for (int m = 0; m < GM; ++m)
       if (ok[m]) {
-        pa[m] += gamma0 * yvec(m);
-        pb[m] += gamma0 * gvec(m);
+        if constexpr (HYD) {
+          pb[m] += gamma0 * gvec(m);
+          pa[m] = pb[m] + *reinterpret_cast<const f4v*>(dprev + 4 * (lane + kWave * m));
+        } else {
+          pa[m] += gamma0 * yvec(m);
+          pb[m] += gamma0 * gvec(m);
+        }
       }
     put(a_out, b_out);
   };
   if constexpr (NW == 1) {
     finish();
+    return;
+  }
+  if constexpr (HYD) {
+    // only H'g partials: w0 (+ w2) into spare0, w1 (+ w3) into spare1; the caller's block-wide
+    // pass adds them, gamma0 g and d_prev (spare2 / spare3 and d stay untouched)
+    auto put1 = [&](float* B) {
+#pragma unroll
+      for (int m = 0; m < GM; ++m)
+        if (ok[m]) *reinterpret_cast<f4v*>(B + 4 * (lane + kWave * m)) = pb[m];
+    };
+    auto add1 = [&](const float* B) {
+#pragma unroll
+      for (int m = 0; m < GM; ++m)
+        if (ok[m]) pb[m] += *reinterpret_cast<const f4v*>(B + 4 * (lane + kWave * m));
+    };
+    if constexpr (NW == 2) {
+      put1(wave == 0 ? spare0 : spare1);
+      return;
+    }
+    if (wave == 2) put1(spare0);
+    if (wave == 3) put1(spare1);
+    __syncthreads();
+    if (wave == 0) { add1(spare0); put1(spare0); }
+    if (wave == 1) { add1(spare1); put1(spare1); }
     return;
   }
   if constexpr (NW == 2) {
@@ -1306,10 +1382,10 @@ __global__ __launch_bounds__(kWave * NW, DAVA_SOLVE_WAVES_PER_EU) void bfgs_ba_s
               else if (GT == 6) compact_products_wide<6, NW>(P, Pv, nh, SH, WH, hrho, hc, gamma0, g, gp, hy_new, hg, scratch, buf);
               else compact_products_wide<7, NW>(P, Pv, nh, SH, WH, hrho, hc, gamma0, g, gp, hy_new, hg, scratch, buf);
             } else
-            if (GM <= 1) compact_products_fused<1, NW>(P, Pv, k - 1, SH, WH, LH, lcap, hrho, hc, gamma0, g, gp, hy_new, hg, s_pend, hy_pend, d, hg);
-            else if (GM == 2) compact_products_fused<2, NW>(P, Pv, k - 1, SH, WH, LH, lcap, hrho, hc, gamma0, g, gp, hy_new, hg, s_pend, hy_pend, d, hg);
-            else if (GM == 3) compact_products_fused<3, NW>(P, Pv, k - 1, SH, WH, LH, lcap, hrho, hc, gamma0, g, gp, hy_new, hg, s_pend, hy_pend, d, hg);
-            else if (GM == 4) compact_products_fused<4, NW>(P, Pv, k - 1, SH, WH, LH, lcap, hrho, hc, gamma0, g, gp, hy_new, hg, s_pend, hy_pend, d, hg);
+            if (GM <= 1) compact_products_fused<1, NW>(P, Pv, k - 1, SH, WH, LH, lcap, hrho, hc, gamma0, g, gp, hy_new, hg, s_pend, hy_pend, d, hg, d);
+            else if (GM == 2) compact_products_fused<2, NW>(P, Pv, k - 1, SH, WH, LH, lcap, hrho, hc, gamma0, g, gp, hy_new, hg, s_pend, hy_pend, d, hg, d);
+            else if (GM == 3) compact_products_fused<3, NW>(P, Pv, k - 1, SH, WH, LH, lcap, hrho, hc, gamma0, g, gp, hy_new, hg, s_pend, hy_pend, d, hg, d);
+            else if (GM == 4) compact_products_fused<4, NW>(P, Pv, k - 1, SH, WH, LH, lcap, hrho, hc, gamma0, g, gp, hy_new, hg, s_pend, hy_pend, d, hg, d);
             else
   #endif
             // GV mode (very long rows, few resident waves): 8 column groups in flight per lane;
@@ -1323,9 +1399,17 @@ __global__ __launch_bounds__(kWave * NW, DAVA_SOLVE_WAVES_PER_EU) void bfgs_ba_s
           if (deferred) {  // finish the fused pass's cross-wave sum here, all threads at once
             for (int i = tid; i < P; i += BLOCK) {
               const float gi = g[i], yi = gi - gp[i], si = s_cur[i];
-              float hi = s_pend[i] + d[i], gh = hy_pend[i] + hg[i];
-              hi += gamma0 * yi;
-              gh += gamma0 * gi;
+              float hi, gh;
+              if constexpr (DAVA_HY_FROM_D_LDS) {  // H'g partials in s_pend / hy_pend; H'y = H'g + d_prev
+                gh = s_pend[i] + hy_pend[i];
+                gh += gamma0 * gi;
+                hi = gh + d[i];
+              } else {
+                hi = s_pend[i] + d[i];
+                gh = hy_pend[i] + hg[i];
+                hi += gamma0 * yi;
+                gh += gamma0 * gi;
+              }
               hy_new[i] = hi;
               hg[i] = gh;
               r[0] += si * yi; r[1] += hi * yi; r[2] += si * gi; r[3] += hi * gi;
