@@ -309,8 +309,11 @@ __device__ __forceinline__ void wide_pair_pass(int P, int Pv, int j0, int j1, co
 // registers of the dual-number evaluation and the kernel ran 39% slower (148.6 -> 206.9 ms at C3).
 // GT > 0: global-vector mode (the O(P) vectors in the workspace slice a.gvws, wide_pair_pass with up
 // to GT float4 groups per thread); GT = 0: everything O(P) in LDS (pair_pass, GM groups per lane).
+#ifndef DAVA_ADJ_LDS_WPE
+#define DAVA_ADJ_LDS_WPE 2  // LDS mode: workgroups per CU (registers <= 256 VGPRs, LDS <= 80 KB each)
+#endif
 template <int RES, int GM, int GT = 0>
-__global__ __launch_bounds__(kAdjBlock, 1) void bfgs_ba_adjoint_kernel(AdjointArgs a) {
+__global__ __launch_bounds__(kAdjBlock, GT > 0 ? 1 : DAVA_ADJ_LDS_WPE) void bfgs_ba_adjoint_kernel(AdjointArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   constexpr bool GVM = GT > 0;
   const Layout L = a.L;
@@ -566,7 +569,7 @@ static int adjoint_check(const DavaScene* s, const DavaSolverConfig* c) {
 static int adjoint_lds_entries(const DavaScene* s, const TapeLayout& tl) {
   if (adjoint_gv(s, tl)) return 0;
   const int base = carve_adjoint(s->num_views, s->num_points, tl.Pv, tl.T).total_bytes;
-  int n = (kAdjLdsBytes - base) / (int)(2 * tl.Pv * sizeof(float));
+  int n = (kAdjLdsBytes / DAVA_ADJ_LDS_WPE - base) / (int)(2 * tl.Pv * sizeof(float));
   n = max(0, min(n, tl.K - 1));
   if (const char* e = getenv("DAVA_ADJ_LDS_ENTRIES")) n = max(0, min(n, atoi(e)));
   return n;
