@@ -71,7 +71,8 @@ struct AdjointCarve {
 // gv (global-vector mode, P too large for the LDS image, e.g. C5): the O(P) vectors are offsets into
 // the problem's workspace slice instead, the scene is read in place and the observation cotangent is
 // accumulated straight into the output; LDS keeps the scalars, view constants and reduction scratch.
-__host__ __device__ inline AdjointCarve carve_adjoint(int M, int N, int Pv, int T, int lcap = 0, bool gv = false) {
+__host__ __device__ inline AdjointCarve carve_adjoint(int M, int N, int Pv, int T, int lcap = 0, bool gv = false,
+                                                     int nw = kAdjWaves) {
   AdjointCarve c;
   int off = 0, voff = 0;
   int& o = gv ? voff : off;
@@ -82,11 +83,11 @@ __host__ __device__ inline AdjointCarve carve_adjoint(int M, int N, int Pv, int 
   c.gd = o; o += 2 * Pv;  // Dual
   c.gv_floats = gv ? voff : 0;
   c.views = off; off += 2 * round_up(views_floats(M), 4);
-  c.vpart = off; off += 2 * round_up(vpart_floats(M, kAdjWaves), 4);
+  c.vpart = off; off += 2 * round_up(vpart_floats(M, nw), 4);
   c.obs = off; off += gv ? 0 : round_up(2 * M * N, 4);
   c.obsacc = off; off += gv ? 0 : round_up(2 * M * N, 4);
   c.lh = off; off += gv ? 0 : 2 * lcap * Pv;
-  c.scratch = off; off += 2 * kAdjWaves * 32;
+  c.scratch = off; off += 2 * nw * 32;
   c.vis_bytes_off = off * 4;
   c.total_bytes = c.vis_bytes_off + (gv ? 0 : round_up(M * N, 16));
   return c;
@@ -231,19 +232,20 @@ __device__ __forceinline__ void pair_pass(int P, int Pv, int j0, int j1, const f
 // of E entries are loaded per round, and one block reduction per round gives every thread the entries'
 // dots in the same order.  R1_j0: entry j0's R1 row from this vector instead of R1 + j0 Pv.  out1 / out2
 // may not alias v1 / v2 of another thread's columns (each thread reads and writes only its own).
-template <int GT, class Coef>
+template <int GT, int NW, class Coef>
 __device__ __forceinline__ void wide_pair_pass(int P, int Pv, int j0, int j1, const float* __restrict__ R1,
                                                const float* __restrict__ R2, const float* v1, const float* v2,
                                                float base, Coef coef, float* out1, float* out2, float* scratch,
                                                int& buf, const float* R1_j0 = nullptr) {
-  constexpr int E = GT <= 8 ? 2 : 1;
+  constexpr int BLOCK = kWave * NW;
+  constexpr int E = GT * NW <= 32 ? 2 : 1;  // two entries per reduction while the rows fit the registers
   const int tid = threadIdx.x;
   const int G = (P + 3) / 4;
   const f4a z = f4a{0, 0, 0, 0};
   f4a a[GT], c[GT], pa[GT], pb[GT];
 #pragma unroll
   for (int u = 0; u < GT; ++u) {
-    const int q = tid + u * kAdjBlock;
+    const int q = tid + u * BLOCK;
     a[u] = c[u] = pa[u] = pb[u] = z;
     if (q < G) {
       a[u] = ldv(v1 + 4 * q);
@@ -259,7 +261,7 @@ __device__ __forceinline__ void wide_pair_pass(int P, int Pv, int j0, int j1, co
       const float* r2p = R2 + (size_t)(j + e) * Pv;
 #pragma unroll
       for (int u = 0; u < GT; ++u) {
-        const int q = tid + u * kAdjBlock;
+        const int q = tid + u * BLOCK;
         r1[e][u] = r2[e][u] = z;
         if (e < ne && q < G) {
           r1[e][u] = ldv(r1p + 4 * q);
@@ -279,7 +281,7 @@ __device__ __forceinline__ void wide_pair_pass(int P, int Pv, int j0, int j1, co
         d[4 * e + 3] += dot4(r2[e][u], c[u]);
       }
     }
-    block_sum<4 * E, kAdjWaves>(d, scratch, buf);
+    block_sum<4 * E, NW>(d, scratch, buf);
     buf ^= 1;
 #pragma unroll
     for (int e = 0; e < E; ++e) {
@@ -296,7 +298,7 @@ __device__ __forceinline__ void wide_pair_pass(int P, int Pv, int j0, int j1, co
   }
 #pragma unroll
   for (int u = 0; u < GT; ++u) {
-    const int q = tid + u * kAdjBlock;
+    const int q = tid + u * BLOCK;
     if (q < G) {
       stv(out1 + 4 * q, pa[u] + base * a[u]);
       stv(out2 + 4 * q, pb[u] + base * c[u]);
@@ -312,15 +314,17 @@ __device__ __forceinline__ void wide_pair_pass(int P, int Pv, int j0, int j1, co
 #ifndef DAVA_ADJ_LDS_WPE
 #define DAVA_ADJ_LDS_WPE 2  // LDS mode: workgroups per CU (registers <= 256 VGPRs, LDS <= 80 KB each)
 #endif
-template <int RES, int GM, int GT = 0>
-__global__ __launch_bounds__(kAdjBlock, GT > 0 ? 1 : DAVA_ADJ_LDS_WPE) void bfgs_ba_adjoint_kernel(AdjointArgs a) {
+template <int RES, int GM, int GT = 0, int NW = kAdjWaves>
+__global__ __launch_bounds__(kWave * NW, GT > 0 ? 1 : DAVA_ADJ_LDS_WPE) void bfgs_ba_adjoint_kernel(AdjointArgs a) {
+  static_assert(GT > 0 || NW == kAdjWaves, "LDS mode (pair_pass) runs four waves");
+  constexpr int BLOCK = kWave * NW;
   extern __shared__ __attribute__((aligned(16))) float lds[];
   constexpr bool GVM = GT > 0;
   const Layout L = a.L;
   const int P = L.P, M = L.M, N = L.N, MN = M * N, Pv = a.Pv, K = a.K;
   const int b = blockIdx.x, tid = threadIdx.x;
   const TapeLayout& tl = a.tl;
-  const AdjointCarve cv = carve_adjoint(M, N, Pv, tl.T, a.lcap, GVM);
+  const AdjointCarve cv = carve_adjoint(M, N, Pv, tl.T, a.lcap, GVM, NW);
   float* vb = GVM ? a.gvws + (size_t)b * cv.gv_floats : lds;  // base of the O(P) vectors
   float* xb = vb + cv.xb;    // xbar: adjoint of x_{k+1} entering step k, of x_k leaving it
   float* sbp = vb + cv.sbp;  // adjoint of s_k from the update that used it (step k + 1)
@@ -364,27 +368,27 @@ __global__ __launch_bounds__(kAdjBlock, GT > 0 ? 1 : DAVA_ADJ_LDS_WPE) void bfgs
   const float* Gr = a.tape + tl.g + (size_t)b * K * Pv;
   float* Ar = a.arows + (size_t)b * K * Pv;
 
-  for (int i = tid; i < Pv; i += kAdjBlock) {
+  for (int i = tid; i < Pv; i += BLOCK) {
     xb[i] = i < P ? a.xbar[(size_t)b * P + i] : 0.f;
     sbp[i] = gbp[i] = anl[i] = 0.f;
   }
-  for (int i = tid; i < tl.T; i += kAdjBlock) sc[i] = a.tape[tl.scal + (size_t)b * tl.T + i];
+  for (int i = tid; i < tl.T; i += BLOCK) sc[i] = a.tape[tl.scal + (size_t)b * tl.T + i];
   if constexpr (GVM) {
     if (obsacc)
-      for (int i = tid; i < 2 * MN; i += kAdjBlock) obsacc[i] = 0.f;
+      for (int i = tid; i < 2 * MN; i += BLOCK) obsacc[i] = 0.f;
   } else {
     float* ol = lds + cv.obs;
     uint8_t* vl = reinterpret_cast<uint8_t*>(lds) + cv.vis_bytes_off;
-    for (int i = tid; i < 2 * MN; i += kAdjBlock) {
+    for (int i = tid; i < 2 * MN; i += BLOCK) {
       ol[i] = a.obs[(size_t)b * 2 * MN + i];
       obsacc[i] = 0.f;
     }
-    for (int i = tid; i < MN; i += kAdjBlock) vl[i] = a.vis[(size_t)b * MN + i] ? 1 : 0;
+    for (int i = tid; i < MN; i += BLOCK) vl[i] = a.vis[(size_t)b * MN + i] ? 1 : 0;
   }
   const int n = min(a.status[(size_t)b * DAVA_STATUS_WORDS], K);
   float* lh = lds + cv.lh;
   const int nlh = GVM ? 0 : min(a.lcap, max(n - 1, 0));  // history entries 0 .. n-2 exist
-  for (int q = tid; q < nlh * (Pv / 4); q += kAdjBlock) {
+  for (int q = tid; q < nlh * (Pv / 4); q += BLOCK) {
     const int j = q / (Pv / 4), i = 4 * (q % (Pv / 4));
     stv(lh + (size_t)2 * j * Pv + i, ldv(S + (size_t)j * Pv + i));
     stv(lh + (size_t)(2 * j + 1) * Pv + i, ldv(W + (size_t)j * Pv + i));
@@ -400,16 +404,16 @@ __global__ __launch_bounds__(kAdjBlock, GT > 0 ? 1 : DAVA_ADJ_LDS_WPE) void bfgs
   for (int k = n - 1; k >= 0; --k) {
     const float alpha = sc[k];
     // ---- s_k = alpha d_k, x_{k+1} = x_k + s_k (alpha is a constant of the line search) ----
-    for (int i = tid; i < Pv; i += kAdjBlock) db[i] = alpha * (xb[i] + sbp[i]);
+    for (int i = tid; i < Pv; i += BLOCK) db[i] = alpha * (xb[i] + sbp[i]);
     if (k == 0) {
-      for (int i = tid; i < Pv; i += kAdjBlock) gk[i] = gbp[i] - db[i];  // d_0 = -g_0
+      for (int i = tid; i < Pv; i += BLOCK) gk[i] = gbp[i] - db[i];  // d_0 = -g_0
     } else {
       const float* gk1 = Gr + (size_t)(k - 1) * Pv;
       const float* gkr = Gr + (size_t)k * Pv;
       const float* srow = S + (size_t)(k - 1) * Pv;
       const float* wrow = W + (size_t)(k - 1) * Pv;
       float* ak = Ar + (size_t)k * Pv;
-      for (int i = tid; i < Pv; i += kAdjBlock) {
+      for (int i = tid; i < Pv; i += BLOCK) {
         const float g1 = i < P ? gkr[i] : 0.f, g0 = i < P ? gk1[i] : 0.f;
         gv[i] = g1;
         yv[i] = g1 - g0;
@@ -425,23 +429,23 @@ __global__ __launch_bounds__(kAdjBlock, GT > 0 ? 1 : DAVA_ADJ_LDS_WPE) void bfgs
         k1 = gs; k2 = as; k3 = gw; k4 = aw;
       };
       if constexpr (GVM) {
-        wide_pair_pass<GT>(P, Pv, k, n, Ar, Gr, sv, wv, 0.f, acoef, p1, p2, scratch, buf, akl);
+        wide_pair_pass<GT, NW>(P, Pv, k, n, Ar, Gr, sv, wv, 0.f, acoef, p1, p2, scratch, buf, akl);
       } else {
         pair_pass<GM>(P, Pv, k, n, Ar, Gr, sv, wv, 0.f, acoef, p1, p2, sp0, sp1, sp2, sp3, akl);
       }
       float r[7] = {0, 0, 0, 0, 0, 0, 0};
-      for (int i = tid; i < P; i += kAdjBlock) {
+      for (int i = tid; i < P; i += BLOCK) {
         const float si = sv[i], wi = wv[i], yi = yv[i], di = db[i];
         r[0] += si * p1[i]; r[1] += si * p2[i]; r[2] += yi * wi; r[3] += si * di; r[4] += wi * di;
         r[5] += yi * yi; r[6] += si * yi;
       }
-      block_sum<7, kAdjWaves>(r, scratch, buf);
+      block_sum<7, NW>(r, scratch, buf);
       buf ^= 1;
       const float sAs = 0.5f * r[0], sAw = r[1], yw = r[2], sd = r[3], wd = r[4], yy = r[5], t = r[6];
       const float cbar = rho * sAs;
       const float rhobar = c * sAs - sAw + cbar * yw;
       const float tbar = rho > 0.f ? -(rho * rho) * rhobar : 0.f;  // inverse_curvature backward
-      for (int i = tid; i < Pv; i += kAdjBlock) {
+      for (int i = tid; i < Pv; i += BLOCK) {
         const float q1 = p1[i], q2 = p2[i];
         wb[i] = -rho * q1 + (cbar * rho) * yv[i];
         p2[i] = (cbar * rho) * wv[i] + tbar * sv[i];  // ybar, direct terms
@@ -458,10 +462,10 @@ __global__ __launch_bounds__(kAdjBlock, GT > 0 ? 1 : DAVA_ADJ_LDS_WPE) void bfgs
           k1 = cr * sdv - rj * wdv; k2 = -rj * sdv;
           k3 = cr * swv - rj * wwv; k4 = -rj * swv;
         };
-        if constexpr (GVM) wide_pair_pass<GT>(P, Pv, 0, k - 1, S, W, db, wb, gamma, hcoef, hd, hw, scratch, buf);
+        if constexpr (GVM) wide_pair_pass<GT, NW>(P, Pv, 0, k - 1, S, W, db, wb, gamma, hcoef, hd, hw, scratch, buf);
         else pair_pass<GM>(P, Pv, 0, k - 1, S, W, db, wb, gamma, hcoef, hd, hw, sp0, sp1, sp2, sp3, nullptr, lh, nlh);
       } else {
-        for (int i = tid; i < Pv; i += kAdjBlock) {
+        for (int i = tid; i < Pv; i += BLOCK) {
           hd[i] = gamma * db[i];
           hw[i] = gamma * wb[i];
         }
@@ -470,7 +474,7 @@ __global__ __launch_bounds__(kAdjBlock, GT > 0 ? 1 : DAVA_ADJ_LDS_WPE) void bfgs
       const float e1 = c * rho * sd - rho * wd, e2 = -rho * sd;
       float tr[1] = {0.f};
       const float* g0r = k == 1 ? Gr : nullptr;
-      for (int i = tid; i < Pv; i += kAdjBlock) {
+      for (int i = tid; i < Pv; i += BLOCK) {
         const float ybar = p2[i] + hw[i];
         const float hk = hd[i] + e1 * sv[i] + e2 * wv[i];
         gk[i] = gbp[i] - hk + ybar;
@@ -481,7 +485,7 @@ __global__ __launch_bounds__(kAdjBlock, GT > 0 ? 1 : DAVA_ADJ_LDS_WPE) void bfgs
         tr[0] += af * gv[i];
         if (k == 1 && i < P) tr[0] -= wb[i] * g0r[i];  // a_0 = -wbar_1
       }
-      block_sum<1, kAdjWaves>(tr, scratch, buf);
+      block_sum<1, NW>(tr, scratch, buf);
       buf ^= 1;
       trace += tr[0];
       if (k == 1) {
@@ -491,7 +495,7 @@ __global__ __launch_bounds__(kAdjBlock, GT > 0 ? 1 : DAVA_ADJ_LDS_WPE) void bfgs
         const float qbar = q >= 1e-4f ? trace : 0.f;  // clamp backward passes where input >= min
         const float tg = qbar / yyc;
         const float yybar = yy >= 1e-5f ? -qbar * q / yyc : 0.f;
-        for (int i = tid; i < Pv; i += kAdjBlock) {
+        for (int i = tid; i < Pv; i += BLOCK) {
           const float extra = tg * sv[i] + 2.0f * yybar * yv[i];
           sbp[i] += tg * yv[i];
           gk[i] += extra;
@@ -501,39 +505,53 @@ __global__ __launch_bounds__(kAdjBlock, GT > 0 ? 1 : DAVA_ADJ_LDS_WPE) void bfgs
     }
     // ---- g_k = dE/dx(x_k): xbar += Hess E gbar_k, obsbar += (d2E/dobs dx) gbar_k ----
     const float* xk = X + (size_t)k * Pv;
-    for (int i = tid; i < Pv; i += kAdjBlock) {
+    for (int i = tid; i < Pv; i += BLOCK) {
       xd[i] = Dual(i < P ? xk[i] : 0.f, i < P ? gk[i] : 0.f);
       gd[i] = Dual(0.f);
     }
     __syncthreads();
     Dual E(0.f), unused(0.f);
 #ifndef DAVA_ADJ_DIAG_NO_HVP  // timing-only diagnostic builds: skip the dual-number evaluation (wrong results)
-    ba_eval<true, false, false, false, false, RES, Dual, kAdjWaves>(L, xd, nullptr, 0.f, obs, vis, gd, views, vpart,
+    ba_eval<true, false, false, false, false, RES, Dual, NW>(L, xd, nullptr, 0.f, obs, vis, gd, views, vpart,
                                                                    scratch, buf, E, unused, nullptr, obsacc);
 #endif
-    for (int i = tid; i < P; i += kAdjBlock) xb[i] += gd[i].t;
+    for (int i = tid; i < P; i += BLOCK) xb[i] += gd[i].t;
     __syncthreads();
   }
-  for (int i = tid; i < P; i += kAdjBlock) a.x0_grad[(size_t)b * P + i] = xb[i];
+  for (int i = tid; i < P; i += BLOCK) a.x0_grad[(size_t)b * P + i] = xb[i];
   if (a.obs_grad && !GVM)
-    for (int i = tid; i < 2 * MN; i += kAdjBlock) a.obs_grad[(size_t)b * 2 * MN + i] = obsacc[i];
+    for (int i = tid; i < 2 * MN; i += BLOCK) a.obs_grad[(size_t)b * 2 * MN + i] = obsacc[i];
+}
+
+// Global-vector mode: waves per workgroup (one workgroup per CU).  Eight: the row passes hold up to 7
+// float4 groups per thread and two waves per SIMD hide their latency; the dual-number evaluation then
+// runs at the 256-VGPR budget.  Four: up to 14 groups per thread, one wave per SIMD with 512 registers.
+#ifndef DAVA_ADJ_GV_WAVES
+#define DAVA_ADJ_GV_WAVES 8
+#endif
+static int adjoint_gv_waves() {
+  if (const char* e = getenv("DAVA_ADJ_GV_WAVES")) return atoi(e) == 4 ? 4 : 8;  // A/B knob
+  return DAVA_ADJ_GV_WAVES;
 }
 
 template <int RES>
-static void launch_adjoint(const AdjointArgs& a, int B, int lds, int gm, int gt, hipStream_t s) {
-  auto go = [&](auto kernel) {
+static void launch_adjoint(const AdjointArgs& a, int B, int lds, int gm, int gt, int nw, hipStream_t s) {
+  auto go = [&](auto kernel, int threads) {
     if (lds > 64 * 1024)
       (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-    hipLaunchKernelGGL(kernel, dim3(B), dim3(kAdjBlock), lds, s, a);
+    hipLaunchKernelGGL(kernel, dim3(B), dim3(threads), lds, s, a);
   };
-  if (gt > 0) {  // global-vector mode: 4, 8 or 14 float4 groups per thread
-    if (gt <= 4) go(bfgs_ba_adjoint_kernel<RES, 1, 4>);
-    else if (gt <= 8) go(bfgs_ba_adjoint_kernel<RES, 1, 8>);
-    else go(bfgs_ba_adjoint_kernel<RES, 1, kAdjMaxGroups>);
-  } else if (gm <= 1) go(bfgs_ba_adjoint_kernel<RES, 1>);
-  else if (gm == 2) go(bfgs_ba_adjoint_kernel<RES, 2>);
-  else if (gm == 3) go(bfgs_ba_adjoint_kernel<RES, 3>);
-  else go(bfgs_ba_adjoint_kernel<RES, 4>);
+  if (gt > 0 && nw == 8) {  // global-vector mode, eight waves: 4 or 7 float4 groups per thread
+    if (gt <= 4) go(bfgs_ba_adjoint_kernel<RES, 1, 4, 8>, 8 * kWave);
+    else go(bfgs_ba_adjoint_kernel<RES, 1, 7, 8>, 8 * kWave);
+  } else if (gt > 0) {  // global-vector mode, four waves: 4, 8 or 14 float4 groups per thread
+    if (gt <= 4) go(bfgs_ba_adjoint_kernel<RES, 1, 4>, kAdjBlock);
+    else if (gt <= 8) go(bfgs_ba_adjoint_kernel<RES, 1, 8>, kAdjBlock);
+    else go(bfgs_ba_adjoint_kernel<RES, 1, kAdjMaxGroups>, kAdjBlock);
+  } else if (gm <= 1) go(bfgs_ba_adjoint_kernel<RES, 1>, kAdjBlock);
+  else if (gm == 2) go(bfgs_ba_adjoint_kernel<RES, 2>, kAdjBlock);
+  else if (gm == 3) go(bfgs_ba_adjoint_kernel<RES, 3>, kAdjBlock);
+  else go(bfgs_ba_adjoint_kernel<RES, 4>, kAdjBlock);
 }
 
 constexpr int kAdjLdsBytes = 160 * 1024;
@@ -628,11 +646,12 @@ extern "C" int dava_ba_solve_backward(const DavaScene* scene, const DavaSolverCo
   a.arows = static_cast<float*>(workspace);
   a.gvws = gv ? reinterpret_cast<float*>(static_cast<char*>(workspace) + rows) : nullptr;
   a.lcap = adjoint_lds_entries(scene, tl);
-  const int lds = carve_adjoint(scene->num_views, scene->num_points, tl.Pv, tl.T, a.lcap, gv).total_bytes;
+  const int nw = gv ? adjoint_gv_waves() : kAdjWaves;
+  const int lds = carve_adjoint(scene->num_views, scene->num_points, tl.Pv, tl.T, a.lcap, gv, nw).total_bytes;
   const int gm = (tl.Pv / 4 + kWave - 1) / kWave;
-  const int gt = gv ? adjoint_groups(tl) : 0;
+  const int gt = gv ? (tl.Pv / 4 + kWave * nw - 1) / (kWave * nw) : 0;  // float4 groups per thread
   hipStream_t s = static_cast<hipStream_t>(stream);
-  if (scene->residual == DAVA_RESIDUAL_RAY_ANGLE) launch_adjoint<DAVA_RESIDUAL_RAY_ANGLE>(a, scene->batch, lds, gm, gt, s);
-  else launch_adjoint<DAVA_RESIDUAL_SQUARED_REPROJECTION>(a, scene->batch, lds, gm, gt, s);
+  if (scene->residual == DAVA_RESIDUAL_RAY_ANGLE) launch_adjoint<DAVA_RESIDUAL_RAY_ANGLE>(a, scene->batch, lds, gm, gt, nw, s);
+  else launch_adjoint<DAVA_RESIDUAL_SQUARED_REPROJECTION>(a, scene->batch, lds, gm, gt, nw, s);
   return hipGetLastError() == hipSuccess ? DAVA_OK : DAVA_ERR_LAUNCH;
 }
