@@ -50,6 +50,7 @@ struct AdjointArgs {
   float* arows;       // (B, K, Pv) workspace
   int lcap;           // history entries (s_j, w_j), j < lcap, held in LDS for the H passes
   float* gvws;        // global-vector mode: (B, kAdjGvFloats(Pv)) per-problem vector slices, else null
+  int gd_lds;         // global-vector mode: the HVP's dual gradient vector in LDS (carve_adjoint gdl)
 };
 
 constexpr int kAdjWaves = 4;
@@ -71,8 +72,10 @@ struct AdjointCarve {
 // gv (global-vector mode, P too large for the LDS image, e.g. C5): the O(P) vectors are offsets into
 // the problem's workspace slice instead, the scene is read in place and the observation cotangent is
 // accumulated straight into the output; LDS keeps the scalars, view constants and reduction scratch.
+// gdl (global-vector mode): the dual gradient vector of the HVP evaluation in LDS instead of the slice
+// -- the evaluation accumulates it view after view, one dependent read-modify-write per pair.
 __host__ __device__ inline AdjointCarve carve_adjoint(int M, int N, int Pv, int T, int lcap = 0, bool gv = false,
-                                                     int nw = kAdjWaves) {
+                                                     int nw = kAdjWaves, bool gdl = false) {
   AdjointCarve c;
   int off = 0, voff = 0;
   int& o = gv ? voff : off;
@@ -80,7 +83,8 @@ __host__ __device__ inline AdjointCarve carve_adjoint(int M, int N, int Pv, int 
   for (int* v : vec) { *v = o; o += Pv; }
   c.sc = off; off += T;
   c.xd = o; o += 2 * Pv;  // Dual
-  c.gd = o; o += 2 * Pv;  // Dual
+  int& og = gv && gdl ? off : o;
+  c.gd = og; og += 2 * Pv;  // Dual
   c.gv_floats = gv ? voff : 0;
   c.views = off; off += 2 * round_up(views_floats(M), 4);
   c.vpart = off; off += 2 * round_up(vpart_floats(M, nw), 4);
@@ -324,7 +328,7 @@ __global__ __launch_bounds__(kWave * NW, GT > 0 ? 1 : DAVA_ADJ_LDS_WPE) void bfg
   const int P = L.P, M = L.M, N = L.N, MN = M * N, Pv = a.Pv, K = a.K;
   const int b = blockIdx.x, tid = threadIdx.x;
   const TapeLayout& tl = a.tl;
-  const AdjointCarve cv = carve_adjoint(M, N, Pv, tl.T, a.lcap, GVM, NW);
+  const AdjointCarve cv = carve_adjoint(M, N, Pv, tl.T, a.lcap, GVM, NW, GVM && a.gd_lds);
   float* vb = GVM ? a.gvws + (size_t)b * cv.gv_floats : lds;  // base of the O(P) vectors
   float* xb = vb + cv.xb;    // xbar: adjoint of x_{k+1} entering step k, of x_k leaving it
   float* sbp = vb + cv.sbp;  // adjoint of s_k from the update that used it (step k + 1)
@@ -353,7 +357,7 @@ __global__ __launch_bounds__(kWave * NW, GT > 0 ? 1 : DAVA_ADJ_LDS_WPE) void bfg
   float* anl = vb + cv.an;
   float* sc = lds + cv.sc;
   Dual* xd = reinterpret_cast<Dual*>(vb + cv.xd);
-  Dual* gd = reinterpret_cast<Dual*>(vb + cv.gd);
+  Dual* gd = reinterpret_cast<Dual*>((GVM && a.gd_lds ? lds : vb) + cv.gd);
   Dual* views = reinterpret_cast<Dual*>(lds + cv.views);
   Dual* vpart = reinterpret_cast<Dual*>(lds + cv.vpart);
   const float* obs = GVM ? a.obs + (size_t)b * 2 * MN : lds + cv.obs;
@@ -647,7 +651,10 @@ extern "C" int dava_ba_solve_backward(const DavaScene* scene, const DavaSolverCo
   a.gvws = gv ? reinterpret_cast<float*>(static_cast<char*>(workspace) + rows) : nullptr;
   a.lcap = adjoint_lds_entries(scene, tl);
   const int nw = gv ? adjoint_gv_waves() : kAdjWaves;
-  const int lds = carve_adjoint(scene->num_views, scene->num_points, tl.Pv, tl.T, a.lcap, gv, nw).total_bytes;
+  a.gd_lds = gv && !getenv("DAVA_ADJ_GD_HBM") &&
+             carve_adjoint(scene->num_views, scene->num_points, tl.Pv, tl.T, a.lcap, gv, nw, true).total_bytes <=
+                 kAdjLdsBytes;
+  const int lds = carve_adjoint(scene->num_views, scene->num_points, tl.Pv, tl.T, a.lcap, gv, nw, a.gd_lds).total_bytes;
   const int gm = (tl.Pv / 4 + kWave - 1) / kWave;
   const int gt = gv ? (tl.Pv / 4 + kWave * nw - 1) / (kWave * nw) : 0;  // float4 groups per thread
   hipStream_t s = static_cast<hipStream_t>(stream);
