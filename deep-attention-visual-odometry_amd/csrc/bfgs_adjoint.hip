@@ -54,6 +54,9 @@ struct AdjointArgs {
 };
 
 constexpr int kAdjWaves = 4;
+#ifndef DAVA_ADJ_PRIO
+#define DAVA_ADJ_PRIO 0
+#endif
 #ifndef DAVA_ADJ_INFLIGHT
 #define DAVA_ADJ_INFLIGHT 2  // 4 and 8 measured no faster / 10% slower at C3
 #endif
@@ -163,8 +166,9 @@ __device__ __forceinline__ void pair_pass(int P, int Pv, int j0, int j1, const f
       pb[m] += k3 * r1[m] + k4 * r2[m];
     }
   };
-  // EF entries of this wave in flight: at one wave per SIMD (the dual evaluation needs > 256
-  // registers) the streams are latency-bound, and the register file has room for the rows
+  // EF entries of this wave in flight (kAdjInflight).  DAVA_ADJ_PRIO: the streaming wave drops to
+  // priority 0, so the other workgroup's dual evaluation issues first (as the forward's history pass)
+  if (DAVA_ADJ_PRIO) __builtin_amdgcn_s_setprio(0);
   int j = j0 + wave;
   for (const int je = min(nl, j1); j < je; j += kAdjWaves) {  // LDS-held entries (wave-uniform)
     f4a r1[GM], r2[GM];
@@ -189,6 +193,7 @@ __device__ __forceinline__ void pair_pass(int P, int Pv, int j0, int j1, const f
     load(j, r1, r2);
     consume(j, r1, r2);
   }
+  if (DAVA_ADJ_PRIO) __builtin_amdgcn_s_setprio(2);
   auto put = [&](float* A, float* B) {
 #pragma unroll
     for (int m = 0; m < GM; ++m)
@@ -321,6 +326,7 @@ __device__ __forceinline__ void wide_pair_pass(int P, int Pv, int j0, int j1, co
 template <int RES, int GM, int GT = 0, int NW = kAdjWaves>
 __global__ __launch_bounds__(kWave * NW, GT > 0 ? 1 : DAVA_ADJ_LDS_WPE) void bfgs_ba_adjoint_kernel(AdjointArgs a) {
   static_assert(GT > 0 || NW == kAdjWaves, "LDS mode (pair_pass) runs four waves");
+  if (DAVA_ADJ_PRIO && GT == 0) __builtin_amdgcn_s_setprio(2);
   constexpr int BLOCK = kWave * NW;
   extern __shared__ __attribute__((aligned(16))) float lds[];
   constexpr bool GVM = GT > 0;
