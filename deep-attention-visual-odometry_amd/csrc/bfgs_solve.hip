@@ -175,8 +175,10 @@ __device__ __forceinline__ f4v buf_ld4(__amdgpu_buffer_rsrc_t r, int voff) {
 #ifndef DAVA_GV_BUFFER_LOADS
 #define DAVA_GV_BUFFER_LOADS 0  // 1: GV wide pass rows through buffer loads (bitwise equal; C5 -2.5 .. +1.8%, not enabled)
 #endif
-#ifndef DAVA_FUSED_BUFFER_LOADS
-#define DAVA_FUSED_BUFFER_LOADS 0  // 1: LDS-mode fused pass rows through buffer loads (bitwise equal; C2 +1-3%, C3 -6%)
+#ifndef DAVA_FUSED_BUFFER_LOADS_GM
+// LDS-mode fused pass: rows of at most this many float4 groups per lane through buffer loads (bitwise
+// equal; all rows, i.e. 4: C3 -6%, profiles/r03_ab_buffer_loads.log; rows of <= 2 groups: C2 +2.5%, C3 +-0.2%)
+#define DAVA_FUSED_BUFFER_LOADS_GM 2  // C1, C2 (profiles/r03_ab_fused_buffer_loads_small.log)
 #endif
 
 #ifndef DAVA_SWEEP_ROWS
@@ -975,32 +977,32 @@ __device__ __forceinline__ void compact_products_fused(int P, int Pv, int nh, co
 #endif
     }
   };
-#if DAVA_FUSED_BUFFER_LOADS
-  // buffer loads: a descriptor per row (range = the row), lane offsets loop-invariant, the groups
-  // past P read zeros through the range check instead of an exec-mask branch (bitwise equal)
+  // buffer loads (rows of <= DAVA_FUSED_BUFFER_LOADS_GM groups per lane): a descriptor per row (range =
+  // the row), lane offsets loop-invariant, the groups past P read zeros through the range check
+  // instead of an exec-mask branch (bitwise equal)
+  constexpr bool kBufferLoads = GM <= DAVA_FUSED_BUFFER_LOADS_GM;
   const float* Su = uniform_ptr(S);
   const float* Wu = uniform_ptr(W);
   auto load = [&](int j, f4v (&s4)[GM], f4v (&w4)[GM]) {
-    const auto rs = make_rsrc(Su + (size_t)j * Pv, 4 * Pv);
-    const auto rw = make_rsrc(Wu + (size_t)j * Pv, 4 * Pv);
+    if constexpr (kBufferLoads) {
+      const auto rs = make_rsrc(Su + (size_t)j * Pv, 4 * Pv);
+      const auto rw = make_rsrc(Wu + (size_t)j * Pv, 4 * Pv);
 #pragma unroll
-    for (int m = 0; m < GM; ++m) {
-      s4[m] = buf_ld4(rs, 16 * (lane + kWave * m));
-      w4[m] = buf_ld4(rw, 16 * (lane + kWave * m));
+      for (int m = 0; m < GM; ++m) {
+        s4[m] = buf_ld4(rs, 16 * (lane + kWave * m));
+        w4[m] = buf_ld4(rw, 16 * (lane + kWave * m));
+      }
+    } else {
+      const float* sr = S + (size_t)j * Pv;
+      const float* wr = W + (size_t)j * Pv;
+#pragma unroll
+      for (int m = 0; m < GM; ++m) {
+        const int q = lane + kWave * m;
+        s4[m] = ok[m] ? *reinterpret_cast<const f4v*>(sr + 4 * q) : f4v{0, 0, 0, 0};
+        w4[m] = ok[m] ? *reinterpret_cast<const f4v*>(wr + 4 * q) : f4v{0, 0, 0, 0};
+      }
     }
   };
-#else
-  auto load = [&](int j, f4v (&s4)[GM], f4v (&w4)[GM]) {
-    const float* sr = S + (size_t)j * Pv;
-    const float* wr = W + (size_t)j * Pv;
-#pragma unroll
-    for (int m = 0; m < GM; ++m) {
-      const int q = lane + kWave * m;
-      s4[m] = ok[m] ? *reinterpret_cast<const f4v*>(sr + 4 * q) : f4v{0, 0, 0, 0};
-      w4[m] = ok[m] ? *reinterpret_cast<const f4v*>(wr + 4 * q) : f4v{0, 0, 0, 0};
-    }
-  };
-#endif
 #if DAVA_HIST_PRIO != DAVA_BASE_PRIO
   __builtin_amdgcn_s_setprio(DAVA_HIST_PRIO);
 #endif
