@@ -55,7 +55,10 @@ struct AdjointArgs {
 
 constexpr int kAdjWaves = 4;
 #ifndef DAVA_ADJ_PRIO
-#define DAVA_ADJ_PRIO 0
+#define DAVA_ADJ_PRIO 0  // 1: row-streaming waves at priority 0 (C3 -1.7%, C2 +1%: profiles/r03_ab_adjoint_prio.log)
+#endif
+#ifndef DAVA_ADJ_BUFFER_LOADS_GM
+#define DAVA_ADJ_BUFFER_LOADS_GM 0  // 2: C1/C2-shape rows through buffer loads (C1 +1%, C2 +-1%: profiles/r03_ab_adjoint_buffer_loads.log)
 #endif
 #ifndef DAVA_ADJ_INFLIGHT
 #define DAVA_ADJ_INFLIGHT 2  // 4 and 8 measured no faster / 10% slower at C3
@@ -142,8 +145,22 @@ __device__ __forceinline__ void pair_pass(int P, int Pv, int j0, int j1, const f
       r2[m] = ok[m] ? ldv(r2p + 4 * q) : f4a{0, 0, 0, 0};
     }
   };
-  auto load = [&](int j, f4a (&r1)[GM], f4a (&r2)[GM]) {  // HBM rows
-    load_from(R1 + (size_t)j * Pv, R2 + (size_t)j * Pv, r1, r2);
+  // HBM rows; rows of <= DAVA_ADJ_BUFFER_LOADS_GM groups per lane through buffer loads (a descriptor
+  // per row with the row as its range: the groups past P read zeros without an exec-masked branch)
+  const float* R1u = uniform_ptr(R1);
+  const float* R2u = uniform_ptr(R2);
+  auto load = [&](int j, f4a (&r1)[GM], f4a (&r2)[GM]) {
+    if constexpr (GM <= DAVA_ADJ_BUFFER_LOADS_GM) {
+      const auto q1 = make_rsrc(R1u + (size_t)j * Pv, 4 * Pv);
+      const auto q2 = make_rsrc(R2u + (size_t)j * Pv, 4 * Pv);
+#pragma unroll
+      for (int m = 0; m < GM; ++m) {
+        r1[m] = buf_ld4(q1, 16 * (lane + kWave * m));
+        r2[m] = buf_ld4(q2, 16 * (lane + kWave * m));
+      }
+    } else {
+      load_from(R1 + (size_t)j * Pv, R2 + (size_t)j * Pv, r1, r2);
+    }
   };
   auto consume = [&](int j, const f4a (&r1)[GM], const f4a (&r2)[GM]) {
     float d11 = 0.f, d21 = 0.f, d12 = 0.f, d22 = 0.f;

@@ -158,20 +158,6 @@ __device__ __forceinline__ f4v pk_fma4(float k, f4v v, f4v c) {
 __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
 __device__ __forceinline__ void st4(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
 
-// Buffer loads (SRD in SGPRs, 32-bit per-lane byte offset): no 64-bit address arithmetic per
-// load, and the descriptor's range check returns zeros past `bytes` with no branch.
-__device__ __forceinline__ const float* uniform_ptr(const float* p) {
-  const unsigned long long v = reinterpret_cast<unsigned long long>(p);
-  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v);
-  const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
-  return reinterpret_cast<const float*>(((unsigned long long)hi << 32) | lo);
-}
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const float* p, int bytes) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p), (short)0, bytes, 0x00020000);
-}
-__device__ __forceinline__ f4v buf_ld4(__amdgpu_buffer_rsrc_t r, int voff) {
-  return __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(r, voff, 0, 0));
-}
 #ifndef DAVA_GV_BUFFER_LOADS
 #define DAVA_GV_BUFFER_LOADS 0  // 1: GV wide pass rows through buffer loads (bitwise equal; C5 -2.5 .. +1.8%, not enabled)
 #endif

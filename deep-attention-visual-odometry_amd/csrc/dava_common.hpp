@@ -127,6 +127,22 @@ __device__ __forceinline__ void block_sum(float (&v)[R], float* scratch, int buf
   }
 }
 
+// Buffer loads (SRD in SGPRs, 32-bit per-lane byte offset): no 64-bit address arithmetic per
+// load, and the descriptor's range check returns zeros past `bytes` with no branch.
+typedef float f4buf __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ const float* uniform_ptr(const float* p) {
+  const unsigned long long v = reinterpret_cast<unsigned long long>(p);
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v);
+  const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
+  return reinterpret_cast<const float*>(((unsigned long long)hi << 32) | lo);
+}
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const float* p, int bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p), (short)0, bytes, 0x00020000);
+}
+__device__ __forceinline__ f4buf buf_ld4(__amdgpu_buffer_rsrc_t r, int voff) {
+  return __builtin_bit_cast(f4buf, __builtin_amdgcn_raw_buffer_load_b128(r, voff, 0, 0));
+}
+
 // Sum of NW per-wave partials stored `stride` apart, in wave order.
 template <int NW, typename T>
 __device__ __forceinline__ T wave_partials_total(const T* p, int stride) {
