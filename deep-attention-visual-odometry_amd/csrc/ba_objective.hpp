@@ -116,6 +116,9 @@ enum ViewField {
 
 // Partial sums per view kept by each wave: 8 floats {gw_direct xyz, g_theta, g_t~ xyz, -}
 constexpr int kViewPart = 8;
+#ifndef DAVA_VIEW_TOTALS
+#define DAVA_VIEW_TOTALS 1  // DOT evaluations: per-view totals summed once (ba_eval, step 5)
+#endif
 
 // LDS footprint helpers (floats)
 __host__ __device__ inline int views_floats(int M) { return (M - 1) * kViewStride; }
@@ -778,12 +781,26 @@ __device__ __forceinline__ bool ba_eval(const Layout& L, const S* x, const S* d,
     const S g_ps = gs * fN / fNM, g_cs = gs * fM / fNM;
     const S gabsX = g_ps / (3.0f * fN);
     const S gabsT = g_cs / (3.0f * (float)(M - 1));
+    // DOT (every thread forms d . grad, which reads all the per-view totals): the 7 (M - 1) totals are
+    // summed once, in parallel, into the reduction half the next block_sum writes (free until then:
+    // its last reads were before this reduction's barrier; the closing barrier below ends these
+    // reads) -- the same sums in the same order, instead of every thread re-adding NW partials each.
+    S* vtot = nullptr;
+    if constexpr (DOT && DAVA_VIEW_TOTALS && std::is_same<S, float>::value) {
+      if (7 * (M - 1) <= NW * 32) {
+        vtot = scratch + buf * (NW * 32);
+        for (int q = tid; q < 7 * (M - 1); q += BLOCK)
+          vtot[q] = wave_partials_total<NW>(vpart + ((1 + q / 7) * NW) * kViewPart + q % 7, kViewPart);
+        __syncthreads();
+      }
+    }
     if constexpr (DOT) {
       // d . grad = (1/s) sum d.gX~ + gabsX sum d.sgn(X) + views + intrinsics (all threads, same order)
       S dv = 0.f;
       for (int m = 1; m < M; ++m) {
         const S* v = views + (m - 1) * kViewStride;
         auto vs = [&](int k) {
+          if (vtot) return vtot[(m - 1) * 7 + k];
           const S* p = vpart + (m * NW) * kViewPart + k;
           return wave_partials_total<NW>(p, kViewPart);
         };
@@ -824,6 +841,7 @@ __device__ __forceinline__ bool ba_eval(const Layout& L, const S* x, const S* d,
       const int m = 1 + q / 6, c = q % 6;
       const S* v = views + (m - 1) * kViewStride;
       auto vsum = [&](int k) {
+        if (vtot) return vtot[(m - 1) * 7 + k];
         const S* p = vpart + (m * NW) * kViewPart + k;
         return wave_partials_total<NW>(p, kViewPart);
       };
