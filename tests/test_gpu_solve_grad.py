@@ -491,6 +491,34 @@ def test_gv_adjoint_matches_lds_adjoint(device, ray, monkeypatch):
     assert rx.max() <= tol and ro.max() <= tol, (rx, ro)
 
 
+@pytest.mark.parametrize("waves,gd_hbm", [("4", False), ("8", True)])
+def test_gv_adjoint_forms_agree(device, waves, gd_hbm, monkeypatch):
+    """The global-vector adjoint's variants -- four waves with 14 groups per thread, and eight waves
+    with the HVP's dual gradient in the workspace instead of LDS -- against the default (eight waves,
+    dual gradient in LDS) on one C3-shaped tape: the same math in another summation order (four vs
+    eight waves) or bit for bit (where the dual gradient lives)."""
+    from deep_attention_visual_odometry_amd import make_scenes
+
+    monkeypatch.setenv("DAVA_ADJ_FORCE_GV", "1")
+    m, n, k = 4, 256, 24
+    s = make_scenes(8, m, n, distortion=True, seed=938, drop=0.0)
+    x0, obs, vis = (torch.tensor(t).to(device) for t in (s.initial, s.observations, s.visibility))
+    vis = vis.to(torch.uint8)
+    w = torch.randn(x0.shape, generator=torch.Generator().manual_seed(7)).to(device)
+    x, status, tape = torch.ops.dava.ba_solve_record(x0, obs, vis, m, n, True, 1e-4, 0.9, -1.0, k, -1.0, 1000, True, 0)
+    assert (status[:, 0] == k).all() and torch.isfinite(x).all()
+    gx, gobs = torch.ops.dava.ba_solve_backward(w, tape, status, obs, vis, m, n, True, k, 0, True)
+    monkeypatch.setenv("DAVA_ADJ_GV_WAVES", waves)
+    if gd_hbm:
+        monkeypatch.setenv("DAVA_ADJ_GD_HBM", "1")
+    gx2, gobs2 = torch.ops.dava.ba_solve_backward(w, tape, status, obs, vis, m, n, True, k, 0, True)
+    if waves == "8":
+        assert torch.equal(gx2, gx) and torch.equal(gobs2, gobs)
+    else:
+        rx, ro = _rows_rel(gx2.cpu(), gx.cpu()), _rows_rel(gobs2.cpu(), gobs.cpu())
+        assert rx.max() <= 1e-4 and ro.max() <= 1e-4, (rx, ro)
+
+
 def test_gv_recording_is_bitwise_the_gv_solve(device, monkeypatch):
     """A global-vector-mode recording (DAVA_FORCE_GV at the C3 shape: the forward's vectors in the
     tape's own region, wide history pass writing the tape rows) returns exactly the GV solve's x and
