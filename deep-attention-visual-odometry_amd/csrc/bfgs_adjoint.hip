@@ -61,7 +61,7 @@ constexpr int kAdjWaves = 4;
 #define DAVA_ADJ_BUFFER_LOADS_GM 0  // 2: C1/C2-shape rows through buffer loads (C1 +1%, C2 +-1%: profiles/r03_ab_adjoint_buffer_loads.log)
 #endif
 #ifndef DAVA_ADJ_INFLIGHT
-#define DAVA_ADJ_INFLIGHT 2  // 4 and 8 measured no faster / 10% slower at C3
+#define DAVA_ADJ_INFLIGHT 2  // at two workgroups per CU: 1 and 3 slower (profiles/r03_ab_adjoint_inflight.log)
 #endif
 constexpr int kAdjInflight = DAVA_ADJ_INFLIGHT;  // entries per wave in flight in the passes
 constexpr int kAdjBlock = kWave * kAdjWaves;
