@@ -203,13 +203,23 @@ def cpu_baseline(args, x0, obs, vis, x_gpu):
         # per-block envelopes on the first slice: 10x the oracle's own change under a 1-ulp nudge of x0
         # (up and down), floor 1e-5 -- the reference's sensitivity, the bar no fp32 solver can beat
         m = min(args.parity_envelope, n)
-        env = {k: torch.full((m,), PARITY_BAR, dtype=torch.float64) for k in ("x", "i", "d")}
+        spread = {k: torch.zeros((m,), dtype=torch.float64) for k in ("x", "i", "d")}  # the 1x 1-ulp spread
         for to in (float("inf"), -float("inf")):
             nudged = solver.bfgs_solve(torch.nextafter(x0[:m], torch.full_like(x0[:m], to)), closure(0, m), **kw)
             for key, sl in (("x", slice(None)), ("i", slice(0, 3)), ("d", slice(-5, None))):
-                env[key] = torch.maximum(env[key], 10.0 * _rel(nudged[:, sl], ref[:m, sl]))
+                spread[key] = torch.maximum(spread[key], _rel(nudged[:, sl], ref[:m, sl]))
+        env = {k: torch.clamp(10.0 * v, min=PARITY_BAR) for k, v in spread.items()}
         rel_d = _rel(gpu[:, -5:], ref[:, -5:])
+
+        def over(r, k):  # the GPU's distance in units of the reference's own 1-ulp spread (floor: 1 ulp of it)
+            q = r[:m] / torch.clamp(spread[k], min=1e-300)
+            return {"max": float(q.max()), "median": float(q.median())}
+
         parity.update({
+            "whole_max_rel_over_1ulp": over(rel, "x"),
+            "intrinsics_max_rel_over_1ulp": over(rel_i, "i"),
+            "distortion_max_rel_over_1ulp": over(rel_d, "d"),
+            "distortion_spread_1ulp_max": float(spread["d"].max()),
             "distortion_max_rel": float(rel_d.max()),
             "distortion_frac_le_bar": float((rel_d <= PARITY_BAR).double().mean()),
             "envelope_problems": m,
@@ -219,7 +229,9 @@ def cpu_baseline(args, x0, obs, vis, x_gpu):
             "distortion_envelope_max": float(env["d"].max()),
             "distortion_envelope_min": float(env["d"].min()),
             "distortion_max_rel_over_envelope": float((rel_d[:m] / env["d"]).max()),
-            "note": ("per-block envelopes = max(1e-5, 10x the oracle's own change under a 1-ulp nudge of x0); the "
+            "note": ("per-block envelopes = max(1e-5, 10x the oracle's own change under a 1-ulp nudge of x0); "
+                     "*_over_1ulp = the GPU's distance / that change (1x, no floor): <= 1 means no farther from the "
+                     "oracle than the reference is from itself under a 1-ulp nudge; the "
                      "oracle's Brown-Conrady path is bitwise the reference's distorted_camera_model._full_forward_model "
                      "(tests/golden/distortion.npz), whose own eager and TorchScript runs differ on k1..p2 by up to "
                      "~1e-3 at K=100"),

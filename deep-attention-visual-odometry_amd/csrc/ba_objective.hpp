@@ -29,10 +29,6 @@
 
 #include <type_traits>
 
-#ifndef DAVA_Z_NUDGE
-#define DAVA_Z_NUDGE 1  // the distorted model's z' == 0 -> 1e-8 nudge (0: A/B builds only)
-#endif
-
 namespace dava {
 
 // Diagnostic builds only (DAVA_PHASE_TIMING): thread 0 of every workgroup adds the shader
@@ -60,10 +56,6 @@ __device__ unsigned long long g_eval_cycles[kEvalSections];
 // Two points' worth of fp32 in one register pair: the packed pair sweep (PACK) runs the
 // per-(view, point) arithmetic on v_pk_{fma,mul,add}_f32, two points per instruction.
 typedef float pf2 __attribute__((ext_vector_type(2)));
-#ifndef DAVA_PREFETCH_SCENE
-#define DAVA_PREFETCH_SCENE 0  // 1: load the next point pair's observations one step ahead (C5 -7%: registers,
-                               // profiles/r02_ab_prefetch_c5.log)
-#endif
 
 struct Layout {
   int M, N, P, distort;
@@ -116,9 +108,6 @@ enum ViewField {
 
 // Partial sums per view kept by each wave: 8 floats {gw_direct xyz, g_theta, g_t~ xyz, -}
 constexpr int kViewPart = 8;
-#ifndef DAVA_VIEW_TOTALS
-#define DAVA_VIEW_TOTALS 1  // DOT evaluations: per-view totals summed once (ba_eval, step 5)
-#endif
 
 // LDS footprint helpers (floats)
 __host__ __device__ inline int views_floats(int M) { return (M - 1) * kViewStride; }
@@ -149,20 +138,16 @@ struct RayAngle {
 };
 constexpr float kRayEps = 2.220446049250313e-16f;
 
-// DAVA_RAY_RCP: divide by a norm as a multiplication by its reciprocal (one IEEE division per norm
-// instead of one per component: ~16 -> 7 division sequences per (view, point) pair).  Results move
-// by an ulp against torch's per-component division; 0 restores the component-wise form.
-#ifndef DAVA_RAY_RCP
-#define DAVA_RAY_RCP 1
-#endif
-// unit vector x / clamp(|x|, eps) and the projection of a cotangent / tangent through it
-// (inv_n = 1 / n, used when DAVA_RAY_RCP)
+// Every division by a norm is a multiplication by its reciprocal (one IEEE division per norm instead
+// of one per component: ~16 -> 7 division sequences per (view, point) pair; C3 ray 180k -> 204k
+// problems/s, profiles/r02_ab_ray_rcp.log).  Results move by an ulp against torch's per-component
+// division; every ray-angle parity test is unchanged.
+// unit vector x / clamp(|x|, eps) and the projection of a cotangent / tangent through it (inv_n = 1 / n)
 template <typename S>
-__device__ __forceinline__ void ray_unit_backward(S r, S n, S inv_n, const S (&u)[3], const S (&g)[3],
-                                                  S (&out)[3]) {
+__device__ __forceinline__ void ray_unit_backward(S r, S inv_n, const S (&u)[3], const S (&g)[3], S (&out)[3]) {
   const S k = r >= kRayEps ? u[0] * g[0] + u[1] * g[1] + u[2] * g[2] : S(0.0f);
 #pragma unroll
-  for (int c = 0; c < 3; ++c) out[c] = DAVA_RAY_RCP ? (g[c] - u[c] * k) * inv_n : (g[c] - u[c] * k) / n;
+  for (int c = 0; c < 3; ++c) out[c] = (g[c] - u[c] * k) * inv_n;
 }
 
 template <bool GRAD, bool SLOPE, typename S>
@@ -175,11 +160,9 @@ __device__ __forceinline__ void ray_angle_pair(const RayAngle<S>& ra, const floa
   const S hn = clamp_min(hr, kRayEps);
   const S pr = sqrt_(p0 * p0 + p1 * p1 + p2 * p2);
   const S pn = clamp_min(pr, kRayEps);
-  const S ihn = DAVA_RAY_RCP ? 1.0f / hn : S(0.0f), ipn = DAVA_RAY_RCP ? 1.0f / pn : S(0.0f);
-  const S a[3] = {DAVA_RAY_RCP ? h[0] * ihn : h[0] / hn, DAVA_RAY_RCP ? h[1] * ihn : h[1] / hn,
-                  DAVA_RAY_RCP ? h[2] * ihn : h[2] / hn};
-  const S b[3] = {DAVA_RAY_RCP ? p0 * ipn : p0 / pn, DAVA_RAY_RCP ? p1 * ipn : p1 / pn,
-                  DAVA_RAY_RCP ? p2 * ipn : p2 / pn};
+  const S ihn = 1.0f / hn, ipn = 1.0f / pn;
+  const S a[3] = {h[0] * ihn, h[1] * ihn, h[2] * ihn};
+  const S b[3] = {p0 * ipn, p1 * ipn, p2 * ipn};
   const S su[3] = {a[0] + b[0], a[1] + b[1], a[2] + b[2]};
   const S df[3] = {a[0] - b[0], a[1] - b[1], a[2] - b[2]};
   const S Sn = sqrt_(su[0] * su[0] + su[1] * su[1] + su[2] * su[2]);
@@ -187,31 +170,31 @@ __device__ __forceinline__ void ray_angle_pair(const RayAngle<S>& ra, const floa
   e += 2.0f * atan2_(Dn, Sn) * wgt;
   const S den = Sn * Sn + Dn * Dn;
   // reciprocals shared by the forward (slope) and reverse (gradient) parts
-  const S iden = DAVA_RAY_RCP && (GRAD || SLOPE) ? 1.0f / den : S(0.0f);
-  const S iSn = DAVA_RAY_RCP && (GRAD || SLOPE) && Sn > 0.0f ? 1.0f / Sn : S(0.0f);
-  const S iDn = DAVA_RAY_RCP && (GRAD || SLOPE) && Dn > 0.0f ? 1.0f / Dn : S(0.0f);
+  const S iden = (GRAD || SLOPE) ? 1.0f / den : S(0.0f);
+  const S iSn = (GRAD || SLOPE) && Sn > 0.0f ? 1.0f / Sn : S(0.0f);
+  const S iDn = (GRAD || SLOPE) && Dn > 0.0f ? 1.0f / Dn : S(0.0f);
   if constexpr (SLOPE) {
     const S dh[3] = {-ra.dcx, -ra.dcy, ra.dF};
     const S dp[3] = {dp0, dp1, dp2};
     S da[3], db[3];
-    ray_unit_backward(hr, hn, ihn, a, dh, da);  // the Jacobian of x -> x/|x| is symmetric
-    ray_unit_backward(pr, pn, ipn, b, dp, db);
+    ray_unit_backward(hr, ihn, a, dh, da);  // the Jacobian of x -> x/|x| is symmetric
+    ray_unit_backward(pr, ipn, b, dp, db);
     const S nS = su[0] * (da[0] + db[0]) + su[1] * (da[1] + db[1]) + su[2] * (da[2] + db[2]);
     const S nD = df[0] * (da[0] - db[0]) + df[1] * (da[1] - db[1]) + df[2] * (da[2] - db[2]);
-    const S dS = Sn > 0.0f ? (DAVA_RAY_RCP ? nS * iSn : nS / Sn) : S(0.0f);
-    const S dD = Dn > 0.0f ? (DAVA_RAY_RCP ? nD * iDn : nD / Dn) : S(0.0f);
-    sl += DAVA_RAY_RCP ? 2.0f * wgt * (Sn * dD - Dn * dS) * iden : 2.0f * wgt * (Sn * dD - Dn * dS) / den;
+    const S dS = Sn > 0.0f ? nS * iSn : S(0.0f);
+    const S dD = Dn > 0.0f ? nD * iDn : S(0.0f);
+    sl += 2.0f * wgt * (Sn * dD - Dn * dS) * iden;
   }
   if constexpr (GRAD) {
-    const S gD = DAVA_RAY_RCP ? 2.0f * wgt * Sn * iden : 2.0f * wgt * Sn / den;  // atan2 backward
-    const S gS = DAVA_RAY_RCP ? -2.0f * wgt * Dn * iden : -2.0f * wgt * Dn / den;
-    const S cD = Dn > 0.0f ? (DAVA_RAY_RCP ? gD * iDn : gD / Dn) : S(0.0f);
-    const S cS = Sn > 0.0f ? (DAVA_RAY_RCP ? gS * iSn : gS / Sn) : S(0.0f);
+    const S gD = 2.0f * wgt * Sn * iden;  // atan2 backward
+    const S gS = -2.0f * wgt * Dn * iden;
+    const S cD = Dn > 0.0f ? gD * iDn : S(0.0f);
+    const S cS = Sn > 0.0f ? gS * iSn : S(0.0f);
     const S ga[3] = {cS * su[0] + cD * df[0], cS * su[1] + cD * df[1], cS * su[2] + cD * df[2]};
     const S gb[3] = {cS * su[0] - cD * df[0], cS * su[1] - cD * df[1], cS * su[2] - cD * df[2]};
     S gh[3], gp[3];
-    ray_unit_backward(hr, hn, ihn, a, ga, gh);
-    ray_unit_backward(pr, pn, ipn, b, gb, gp);
+    ray_unit_backward(hr, ihn, a, ga, gh);
+    ray_unit_backward(pr, ipn, b, gb, gp);
     gin[0] += gh[2] * ra.Fp;
     gin[1] -= gh[0];
     gin[2] -= gh[1];
@@ -444,7 +427,7 @@ __device__ __forceinline__ bool ba_eval(const Layout& L, const S* x, const S* d,
         // projection; the distorted model nudges z' == 0 by 1e-8 (distorted_camera_model.py:57)
         // branch-free: + (-0) leaves every p2 (signed zeros included) bit for bit, so the pinhole
         // model is untouched; a runtime-uniform branch here cost C2 5% (profiles/r03_ab_c2_regression_bisect.log)
-        if constexpr (DAVA_Z_NUDGE) p2 = p2 + (p2 == S(0.0f) ? z_nudge : -0.0f);
+        p2 = p2 + (p2 == S(0.0f) ? z_nudge : -0.0f);
         const S iz = 1.0f / p2;
         const S qx = p0 * iz, qy = p1 * iz;
         const S ub = in.f * qx, vb = in.f * qy;
@@ -562,8 +545,8 @@ __device__ __forceinline__ bool ba_eval(const Layout& L, const S* x, const S* d,
     } else {
       int n0 = tid;
       if constexpr (PACK && RES == DAVA_RESIDUAL_SQUARED_REPROJECTION && std::is_same<S, float>::value) {
-        // the pair's observations and visibility (read in place from HBM in GV mode); with
-        // DAVA_PREFETCH_SCENE the next pair's are loaded before this pair's arithmetic
+        // the pair's observations and visibility (read in place from HBM in GV mode).  (Loading the next
+        // pair's one step ahead measured C5 -7%: registers, profiles/r02_ab_prefetch_c5.log.)
         struct ScenePair {
           pf2 u, v, w;
         };
@@ -612,10 +595,9 @@ __device__ __forceinline__ bool ba_eval(const Layout& L, const S* x, const S* d,
               dp2 = da2 * vc + a2 * dc + k * w2 + Avw * dw2 + e2 * vB + c2 * dB + dtt2;
             }
           }
-          if constexpr (DAVA_Z_NUDGE) {  // z' == 0 nudge (distorted_camera_model.py:57), branch-free
-            p2.x = p2.x + (p2.x == 0.0f ? z_nudge : -0.0f);
-            p2.y = p2.y + (p2.y == 0.0f ? z_nudge : -0.0f);
-          }
+          // z' == 0 nudge (distorted_camera_model.py:57), branch-free
+          p2.x = p2.x + (p2.x == 0.0f ? z_nudge : -0.0f);
+          p2.y = p2.y + (p2.y == 0.0f ? z_nudge : -0.0f);
           const pf2 iz = 1.0f / p2;
           const pf2 qx = p0 * iz, qy = p1 * iz;
           const pf2 ub = in.f * qx, vb = in.f * qy;
@@ -698,17 +680,9 @@ __device__ __forceinline__ bool ba_eval(const Layout& L, const S* x, const S* d,
             }
           }
         };
-        ScenePair next{};
-        if (DAVA_PREFETCH_SCENE && n0 + BLOCK < N) next = fetch(n0, n0 + BLOCK);
         for (; n0 + BLOCK < N; n0 += 2 * BLOCK) {
           const int n1 = n0 + BLOCK, ia = L.pt(n0), ib = L.pt(n1);
-          ScenePair cur;
-          if constexpr (DAVA_PREFETCH_SCENE) {
-            cur = next;
-            if (n0 + 3 * BLOCK < N) next = fetch(n0 + 2 * BLOCK, n0 + 3 * BLOCK);
-          } else {
-            cur = fetch(n0, n1);
-          }
+          const ScenePair cur = fetch(n0, n1);
           pf2 X[3], dX[3] = {0.f, 0.f, 0.f}, q[3] = {0.f, 0.f, 0.f};
 #pragma unroll
           for (int c = 0; c < 3; ++c) {
@@ -744,7 +718,7 @@ __device__ __forceinline__ bool ba_eval(const Layout& L, const S* x, const S* d,
     }
     if constexpr (GRAD) {
       if (m > 0) {
-        if constexpr (std::is_same<S, float>::value && DAVA_TRANSPOSED_SUMS) {
+        if constexpr (std::is_same<S, float>::value) {
           float w[7];
 #pragma unroll
           for (int k = 0; k < 7; ++k) w[k] = vg[k];
@@ -786,7 +760,7 @@ __device__ __forceinline__ bool ba_eval(const Layout& L, const S* x, const S* d,
     // its last reads were before this reduction's barrier; the closing barrier below ends these
     // reads) -- the same sums in the same order, instead of every thread re-adding NW partials each.
     S* vtot = nullptr;
-    if constexpr (DOT && DAVA_VIEW_TOTALS && std::is_same<S, float>::value) {
+    if constexpr (DOT && std::is_same<S, float>::value) {
       if (7 * (M - 1) <= NW * 32) {
         vtot = scratch + buf * (NW * 32);
         for (int q = tid; q < 7 * (M - 1); q += BLOCK)

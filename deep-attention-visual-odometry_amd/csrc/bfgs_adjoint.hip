@@ -30,6 +30,7 @@
 //   xbar += Hess E(x_k) gbar_k,  obsbar += (d2E / dobs dx) gbar_k    (forward-over-reverse, Dual)
 // H_k dbar and H_{k-1} wbar come from one pass over the history rows (s_j, w_j), like the forward's.
 #include "ba_objective.hpp"
+#include "dava_debug.hpp"
 #include "dava_tape.hpp"
 
 namespace dava {
@@ -54,18 +55,14 @@ struct AdjointArgs {
 };
 
 constexpr int kAdjWaves = 4;
-#ifndef DAVA_ADJ_PRIO
-#define DAVA_ADJ_PRIO 0  // 1: row-streaming waves at priority 0 (C3 -1.7%, C2 +1%: profiles/r03_ab_adjoint_prio.log)
-#endif
-#ifndef DAVA_ADJ_BUFFER_LOADS_GM
-#define DAVA_ADJ_BUFFER_LOADS_GM 0  // 2: C1/C2-shape rows through buffer loads (C1 +1%, C2 +-1%: profiles/r03_ab_adjoint_buffer_loads.log)
-#endif
-#ifndef DAVA_ADJ_INFLIGHT
-#define DAVA_ADJ_INFLIGHT 2  // at two workgroups per CU: 1 and 3 slower (profiles/r03_ab_adjoint_inflight.log)
-#endif
-constexpr int kAdjInflight = DAVA_ADJ_INFLIGHT;  // entries per wave in flight in the passes
+// Entries per wave in flight in the passes: at two workgroups per CU, 1 and 3 are slower
+// (profiles/r03_ab_adjoint_inflight.log).  Measured and not kept: the row-streaming waves at
+// priority 0 (C3 -1.7%, C2 +1%, profiles/r03_ab_adjoint_prio.log) and C1/C2-shape rows through
+// buffer loads (C1 +1%, C2 +-1%, profiles/r03_ab_adjoint_buffer_loads.log).
+constexpr int kAdjInflight = 2;
 constexpr int kAdjBlock = kWave * kAdjWaves;
 constexpr int kAdjMaxGroups = 14;  // GV mode: float4 groups per thread (P <= 14 * 256 * 4 = 14336)
+constexpr int kAdjLdsBytes = 160 * 1024;
 
 struct AdjointCarve {
   int xb, sbp, gbp, db, gk, p1, p2, wb, sv, wv, yv, gv, ak, an, sc, xd, gd, views, vpart, obs, obsacc, lh, scratch,
@@ -145,22 +142,9 @@ __device__ __forceinline__ void pair_pass(int P, int Pv, int j0, int j1, const f
       r2[m] = ok[m] ? ldv(r2p + 4 * q) : f4a{0, 0, 0, 0};
     }
   };
-  // HBM rows; rows of <= DAVA_ADJ_BUFFER_LOADS_GM groups per lane through buffer loads (a descriptor
-  // per row with the row as its range: the groups past P read zeros without an exec-masked branch)
-  const float* R1u = uniform_ptr(R1);
-  const float* R2u = uniform_ptr(R2);
+  // HBM rows
   auto load = [&](int j, f4a (&r1)[GM], f4a (&r2)[GM]) {
-    if constexpr (GM <= DAVA_ADJ_BUFFER_LOADS_GM) {
-      const auto q1 = make_rsrc(R1u + (size_t)j * Pv, 4 * Pv);
-      const auto q2 = make_rsrc(R2u + (size_t)j * Pv, 4 * Pv);
-#pragma unroll
-      for (int m = 0; m < GM; ++m) {
-        r1[m] = buf_ld4(q1, 16 * (lane + kWave * m));
-        r2[m] = buf_ld4(q2, 16 * (lane + kWave * m));
-      }
-    } else {
-      load_from(R1 + (size_t)j * Pv, R2 + (size_t)j * Pv, r1, r2);
-    }
+    load_from(R1 + (size_t)j * Pv, R2 + (size_t)j * Pv, r1, r2);
   };
   auto consume = [&](int j, const f4a (&r1)[GM], const f4a (&r2)[GM]) {
     float d11 = 0.f, d21 = 0.f, d12 = 0.f, d22 = 0.f;
@@ -183,9 +167,7 @@ __device__ __forceinline__ void pair_pass(int P, int Pv, int j0, int j1, const f
       pb[m] += k3 * r1[m] + k4 * r2[m];
     }
   };
-  // EF entries of this wave in flight (kAdjInflight).  DAVA_ADJ_PRIO: the streaming wave drops to
-  // priority 0, so the other workgroup's dual evaluation issues first (as the forward's history pass)
-  if (DAVA_ADJ_PRIO) __builtin_amdgcn_s_setprio(0);
+  // EF entries of this wave in flight (kAdjInflight)
   int j = j0 + wave;
   for (const int je = min(nl, j1); j < je; j += kAdjWaves) {  // LDS-held entries (wave-uniform)
     f4a r1[GM], r2[GM];
@@ -210,7 +192,6 @@ __device__ __forceinline__ void pair_pass(int P, int Pv, int j0, int j1, const f
     load(j, r1, r2);
     consume(j, r1, r2);
   }
-  if (DAVA_ADJ_PRIO) __builtin_amdgcn_s_setprio(2);
   auto put = [&](float* A, float* B) {
 #pragma unroll
     for (int m = 0; m < GM; ++m)
@@ -333,17 +314,16 @@ __device__ __forceinline__ void wide_pair_pass(int P, int Pv, int j0, int j1, co
   __syncthreads();
 }
 
-// One workgroup per CU: at two (the C3 image is 78 KB, it would fit) the 256-VGPR cap spills 100-165
-// registers of the dual-number evaluation and the kernel ran 39% slower (148.6 -> 206.9 ms at C3).
+// LDS mode: two workgroups per CU (registers <= 256 VGPRs, LDS <= 80 KB each), so one problem's
+// dual-number evaluation overlaps the other's row passes: C3 solve + gradient 51.7k -> 63.0k problems/s
+// (r03, profiles/r03_ab_adjoint_two_wg_per_cu.log; in r02 the same register cap spilled 100-165
+// registers and one workgroup per CU was faster, since then the passes' register use went down).
 // GT > 0: global-vector mode (the O(P) vectors in the workspace slice a.gvws, wide_pair_pass with up
 // to GT float4 groups per thread); GT = 0: everything O(P) in LDS (pair_pass, GM groups per lane).
-#ifndef DAVA_ADJ_LDS_WPE
-#define DAVA_ADJ_LDS_WPE 2  // LDS mode: workgroups per CU (registers <= 256 VGPRs, LDS <= 80 KB each)
-#endif
+constexpr int kAdjLdsWpe = 2;
 template <int RES, int GM, int GT = 0, int NW = kAdjWaves>
-__global__ __launch_bounds__(kWave * NW, GT > 0 ? 1 : DAVA_ADJ_LDS_WPE) void bfgs_ba_adjoint_kernel(AdjointArgs a) {
+__global__ __launch_bounds__(kWave * NW, GT > 0 ? 1 : kAdjLdsWpe) void bfgs_ba_adjoint_kernel(AdjointArgs a) {
   static_assert(GT > 0 || NW == kAdjWaves, "LDS mode (pair_pass) runs four waves");
-  if (DAVA_ADJ_PRIO && GT == 0) __builtin_amdgcn_s_setprio(2);
   constexpr int BLOCK = kWave * NW;
   extern __shared__ __attribute__((aligned(16))) float lds[];
   constexpr bool GVM = GT > 0;
@@ -538,10 +518,8 @@ __global__ __launch_bounds__(kWave * NW, GT > 0 ? 1 : DAVA_ADJ_LDS_WPE) void bfg
     }
     __syncthreads();
     Dual E(0.f), unused(0.f);
-#ifndef DAVA_ADJ_DIAG_NO_HVP  // timing-only diagnostic builds: skip the dual-number evaluation (wrong results)
     ba_eval<true, false, false, false, false, RES, Dual, NW>(L, xd, nullptr, 0.f, obs, vis, gd, views, vpart,
                                                                    scratch, buf, E, unused, nullptr, obsacc);
-#endif
     for (int i = tid; i < P; i += BLOCK) xb[i] += gd[i].t;
     __syncthreads();
   }
@@ -553,12 +531,11 @@ __global__ __launch_bounds__(kWave * NW, GT > 0 ? 1 : DAVA_ADJ_LDS_WPE) void bfg
 // Global-vector mode: waves per workgroup (one workgroup per CU).  Eight: the row passes hold up to 7
 // float4 groups per thread and two waves per SIMD hide their latency; the dual-number evaluation then
 // runs at the 256-VGPR budget.  Four: up to 14 groups per thread, one wave per SIMD with 512 registers.
-#ifndef DAVA_ADJ_GV_WAVES
-#define DAVA_ADJ_GV_WAVES 8
-#endif
-static int adjoint_gv_waves() {
-  if (const char* e = getenv("DAVA_ADJ_GV_WAVES")) return atoi(e) == 4 ? 4 : 8;  // A/B knob
-  return DAVA_ADJ_GV_WAVES;
+// Eight unless the eight-wave LDS image (per-wave view partials and reduction scratch grow with the
+// waves) does not fit -- many views -- or the kDbgAdjGVWaves override asks for four.
+static int adjoint_gv_waves(const DavaScene* s, const TapeLayout& tl) {
+  if (debug_knob(kDbgAdjGVWaves) == 4) return 4;
+  return carve_adjoint(s->num_views, s->num_points, tl.Pv, tl.T, 0, true, 8).total_bytes <= kAdjLdsBytes ? 8 : 4;
 }
 
 template <int RES>
@@ -581,12 +558,10 @@ static void launch_adjoint(const AdjointArgs& a, int B, int lds, int gm, int gt,
   else go(bfgs_ba_adjoint_kernel<RES, 4>, kAdjBlock);
 }
 
-constexpr int kAdjLdsBytes = 160 * 1024;
-
 // Global-vector mode when the LDS image does not fit one CU (or P > 1024, past pair_pass's 4 groups
-// per lane); DAVA_ADJ_FORCE_GV forces it (tests: the same tape through both kernels).
+// per lane); the kDbgAdjForceGV override forces it (tests: the same tape through both kernels).
 static bool adjoint_gv(const DavaScene* s, const TapeLayout& tl) {
-  if (getenv("DAVA_ADJ_FORCE_GV")) return true;
+  if (debug_flag(kDbgAdjForceGV)) return true;
   return s->num_parameters > 1024 || carve_adjoint(s->num_views, s->num_points, tl.Pv, tl.T).total_bytes > kAdjLdsBytes;
 }
 static int adjoint_groups(const TapeLayout& tl) { return (tl.Pv / 4 + kAdjBlock - 1) / kAdjBlock; }
@@ -603,20 +578,22 @@ static int adjoint_check(const DavaScene* s, const DavaSolverConfig* c) {
   const TapeLayout tl = tape_layout(s->batch, P, c->iterations);
   if (adjoint_gv(s, tl)) {
     if (adjoint_groups(tl) > kAdjMaxGroups) return DAVA_ERR_UNSUPPORTED;
-    if (carve_adjoint(s->num_views, s->num_points, tl.Pv, tl.T, 0, true).total_bytes > kAdjLdsBytes)
+    // the image of the launch that will run: adjoint_gv_waves() falls back to four waves where eight do not fit
+    if (carve_adjoint(s->num_views, s->num_points, tl.Pv, tl.T, 0, true, adjoint_gv_waves(s, tl)).total_bytes >
+        kAdjLdsBytes)
       return DAVA_ERR_UNSUPPORTED;
   }
   return DAVA_OK;
 }
 
 // As many history entries on chip as the CU's LDS leaves room for (one workgroup per CU), at most
-// the K - 1 a solve can make; DAVA_ADJ_LDS_ENTRIES caps it (0: none) for A/B runs.  None in GV mode.
+// the K - 1 a solve can make; the kDbgAdjLdsEntries override caps it (0: none) for A/B runs.  None in GV mode.
 static int adjoint_lds_entries(const DavaScene* s, const TapeLayout& tl) {
   if (adjoint_gv(s, tl)) return 0;
   const int base = carve_adjoint(s->num_views, s->num_points, tl.Pv, tl.T).total_bytes;
-  int n = (kAdjLdsBytes / DAVA_ADJ_LDS_WPE - base) / (int)(2 * tl.Pv * sizeof(float));
+  int n = (kAdjLdsBytes / kAdjLdsWpe - base) / (int)(2 * tl.Pv * sizeof(float));
   n = max(0, min(n, tl.K - 1));
-  if (const char* e = getenv("DAVA_ADJ_LDS_ENTRIES")) n = max(0, min(n, atoi(e)));
+  if (debug_knob(kDbgAdjLdsEntries) >= 0) n = max(0, min(n, (int)debug_knob(kDbgAdjLdsEntries)));
   return n;
 }
 
@@ -673,8 +650,8 @@ extern "C" int dava_ba_solve_backward(const DavaScene* scene, const DavaSolverCo
   a.arows = static_cast<float*>(workspace);
   a.gvws = gv ? reinterpret_cast<float*>(static_cast<char*>(workspace) + rows) : nullptr;
   a.lcap = adjoint_lds_entries(scene, tl);
-  const int nw = gv ? adjoint_gv_waves() : kAdjWaves;
-  a.gd_lds = gv && !getenv("DAVA_ADJ_GD_HBM") &&
+  const int nw = gv ? adjoint_gv_waves(scene, tl) : kAdjWaves;
+  a.gd_lds = gv && !debug_flag(kDbgAdjGdHbm) &&
              carve_adjoint(scene->num_views, scene->num_points, tl.Pv, tl.T, a.lcap, gv, nw, true).total_bytes <=
                  kAdjLdsBytes;
   const int lds = carve_adjoint(scene->num_views, scene->num_points, tl.Pv, tl.T, a.lcap, gv, nw, a.gd_lds).total_bytes;

@@ -23,9 +23,10 @@
 //    never stored (the first sweep synthesises it).
 //  * the line search runs in-kernel; trial slopes come from forward-mode
 //    (JVP) derivatives, gradients at accepted points from reverse mode.
-#include <cstdlib>
+#include <cstring>
 
 #include "ba_objective.hpp"
+#include "dava_debug.hpp"
 #include "dava_tape.hpp"
 
 namespace dava {
@@ -86,15 +87,12 @@ __host__ __device__ constexpr int solve_waves(bool gv) { return gv ? 8 : 4; }
 
 // GV mode, COMPACT: the workgroup-wide single history pass keeps at most this many float4
 // column groups per thread in registers (P <= 7 * 512 * 4 = 14336); longer rows use two passes.
-#ifndef DAVA_WIDE_PASS
-#define DAVA_WIDE_PASS 1
-#endif
 constexpr int kWideMaxGroups = 7;
-#ifndef DAVA_GV_ENTRIES
-#define DAVA_GV_ENTRIES 1  // history entries per block reduction in the wide pass (rows of > 2 groups per thread)
-#endif
+// History entries per block reduction in the wide pass for rows of > 2 groups per thread (two
+// entries' rows do not fit the registers beside y, g and the sums there).
+constexpr int kGvEntries = 1;
 __host__ __device__ inline bool wide_history_pass(int Pv, int kcap, bool gv) {
-  return DAVA_WIDE_PASS && gv && kcap > 0 && (Pv / 4 + kWave * solve_waves(gv) - 1) / (kWave * solve_waves(gv)) <= kWideMaxGroups;
+  return gv && kcap > 0 && (Pv / 4 + kWave * solve_waves(gv) - 1) / (kWave * solve_waves(gv)) <= kWideMaxGroups;
 }
 
 // LDS image of one problem.  In global-vector (GV) mode -- large P, where the O(P)
@@ -143,9 +141,6 @@ __host__ __device__ inline LdsCarve carve_lds(int M, int N, int Pv, int kcap = 0
 typedef float f4v __attribute__((ext_vector_type(4)));
 typedef float f2v __attribute__((ext_vector_type(2)));
 
-#ifndef DAVA_PACKED_HISTORY
-#define DAVA_PACKED_HISTORY 1  // 0: the round-1 history arithmetic (per-element products, wave_sum per dot)
-#endif
 // packed fp32 FMA (v_pk_fma_f32): a * b + c on two lanes of a float pair
 __device__ __forceinline__ f2v pk_fma(f2v a, f2v b, f2v c) { return __builtin_elementwise_fma(a, b, c); }
 // k * v + c on a float4 as two packed FMAs
@@ -158,53 +153,18 @@ __device__ __forceinline__ f4v pk_fma4(float k, f4v v, f4v c) {
 __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
 __device__ __forceinline__ void st4(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
 
-#ifndef DAVA_GV_BUFFER_LOADS
-#define DAVA_GV_BUFFER_LOADS 0  // 1: GV wide pass rows through buffer loads (bitwise equal; C5 -2.5 .. +1.8%, not enabled)
-#endif
-#ifndef DAVA_FUSED_BUFFER_LOADS_GM
-// LDS-mode fused pass: rows of at most this many float4 groups per lane through buffer loads (bitwise
-// equal; all rows, i.e. 4: C3 -6%, profiles/r03_ab_buffer_loads.log; rows of <= 2 groups: C2 +2.5%, C3 +-0.2%)
-#define DAVA_FUSED_BUFFER_LOADS_GM 2  // C1, C2 (profiles/r03_ab_fused_buffer_loads_small.log)
-#endif
-
-#ifndef DAVA_SWEEP_ROWS
-#define DAVA_SWEEP_ROWS 4
-#endif
-#ifndef DAVA_SWEEP_NT
-#define DAVA_SWEEP_NT 0
-#endif
-#ifndef DAVA_DIAG_NO_HBM
-#define DAVA_DIAG_NO_HBM 0
-#endif
-#ifndef DAVA_DIAG_NO_SWEEP
-#define DAVA_DIAG_NO_SWEEP 0
-#endif
-// GV mode (C5: N = 4096 points, eight per thread): the objective's pair sweep takes two points per
-// step on packed fp32 arithmetic (ba_eval PACK).  0: the scalar sweep.
-#ifndef DAVA_PACKED_PAIRS
-#define DAVA_PACKED_PAIRS 1
-#endif
-#ifndef DAVA_TRIAL_DOT
-#define DAVA_TRIAL_DOT 0  // 1: trial slope as d . grad (reverse mode); 0: forward-mode JVP
-#endif
-#ifndef DAVA_TRIAL_DOT_GV
-#define DAVA_TRIAL_DOT_GV 1  // global-vector mode: slope from the gradient (C5 +4%, profiles/r03_ab_c5_dot_hyd.log)
-#endif
-#ifndef DAVA_TRIAL_CHECK
-#define DAVA_TRIAL_CHECK 1  // skip evaluating trial points that round back to x
-#endif
-#ifndef DAVA_DEBUG_TRIALS
-#define DAVA_DEBUG_TRIALS -1  // diagnostic builds: >= 0 prints that problem's line-search trials
-#endif
-#ifndef DAVA_NONFINITE_DOT
-#define DAVA_NONFINITE_DOT 1  // overflowed trials: slope re-formed as grad . d (the reference's class)
-#endif
-#ifndef DAVA_FUSED_PAIR
-#define DAVA_FUSED_PAIR 1  // two history entries in flight per wave (0: one; fewer VGPRs)
-#endif
-#ifndef DAVA_SOLVE_WAVES_PER_EU
-#define DAVA_SOLVE_WAVES_PER_EU 2  // <= 256 VGPRs: two 4-wave workgroups per CU
-#endif
+// LDS-mode fused pass: rows of at most this many float4 groups per lane go through buffer loads (bitwise
+// equal; C1, C2: C2 +2.5%, profiles/r03_ab_fused_buffer_loads_small.log; all rows, i.e. 4: C3 -6%,
+// profiles/r03_ab_buffer_loads.log).  (The GV wide pass through buffer loads: C5 -2.5 .. +1.8% across
+// boxes, not kept.)
+constexpr int kFusedBufferLoadsGM = 2;
+constexpr int kSweepRows = 4;  // DENSE sweep: matrix rows in flight per lane
+// Trial slopes phi'(alpha): forward mode (a JVP riding on the trial's evaluation) in LDS mode, where
+// the reverse-mode form d . grad measured -1% at C3 (profiles/r01b_ab_variants.log, `dot`); d . grad in
+// global-vector mode, where it saves the pair sweep's tangent registers (C5 +4%, r03 interleaved A/B).
+constexpr bool kTrialDotLds = false;
+constexpr bool kTrialDotGv = true;
+constexpr int kSolveWavesPerEU = 2;  // <= 256 VGPRs: two 4-wave workgroups per CU
 // Diagnostic builds only (make variant FLAGS=-DDAVA_PHASE_TIMING=1): thread 0 of every
 // workgroup accumulates shader-clock cycles per solver phase; dava_ba_solve prints the
 // batch averages to stderr after the launch (and synchronises -- never in a product build).
@@ -225,22 +185,11 @@ constexpr int kPhases = 7;  // eval at x, history products, direction, trial eva
   } while (0)
 #endif
 
-// Streaming access to the inverse Hessian: every element is read once and
-// written once per BFGS iteration, never reused by another workgroup.
-__device__ __forceinline__ f4v h_load(const float* p) {
-#if DAVA_SWEEP_NT
-  return __builtin_nontemporal_load(reinterpret_cast<const f4v*>(p));
-#else
-  return *reinterpret_cast<const f4v*>(p);
-#endif
-}
-__device__ __forceinline__ void h_store(float* p, f4v v) {
-#if DAVA_SWEEP_NT
-  __builtin_nontemporal_store(v, reinterpret_cast<f4v*>(p));
-#else
-  *reinterpret_cast<f4v*>(p) = v;
-#endif
-}
+// Streaming access to the inverse Hessian: every element is read once and written once per BFGS
+// iteration, never reused by another workgroup (non-temporal loads and stores measured no better,
+// profiles/r01_ab_sweep_variants.log).
+__device__ __forceinline__ f4v h_load(const float* p) { return *reinterpret_cast<const f4v*>(p); }
+__device__ __forceinline__ void h_store(float* p, f4v v) { *reinterpret_cast<f4v*>(p) = v; }
 
 // Apply the pending rank-2 term to one element (bfgs_solver.py:298-303 order:
 // ((H + (s_rho_i s_j) c) - s_rho_i yH_j) - Hy_i s_rho_j, no FMA contraction).
@@ -263,7 +212,7 @@ template <int NW>
 __device__ __forceinline__ void dense_sweep(const Layout& L, int Pld, float* __restrict__ H, bool materialized, float gamma0,
                             const float* ps, const float* phy, float prho, float pc, const float* g,
                             const float* gp, float* hy_out, float* hg_out) {
-  constexpr int U = DAVA_SWEEP_ROWS;
+  constexpr int U = kSweepRows;
   const int P = L.P;
   const int lane = threadIdx.x & (kWave - 1);
   const int wave = threadIdx.x / kWave;
@@ -293,9 +242,7 @@ __device__ __forceinline__ void dense_sweep(const Layout& L, int Pld, float* __r
         ay[k] += h[k] * yi;
         ag[k] += h[k] * gi;
       }
-#if !DAVA_DIAG_NO_HBM
       if (act) h_store(col + (size_t)r * Pld, h);
-#endif
     };
     auto synth = [&](int r) {  // row r of gamma0 * I restricted to this lane's 4 columns
       f4v h;
@@ -304,9 +251,6 @@ __device__ __forceinline__ void dense_sweep(const Layout& L, int Pld, float* __r
       return h;
     };
     int i = 0;
-#if DAVA_DIAG_NO_HBM  // timing-only build: no matrix traffic (results are wrong)
-    materialized = false;
-#endif
     if (materialized) {
       for (; i + U <= P; i += U) {
         f4v h[U];
@@ -423,7 +367,7 @@ __device__ __forceinline__ void compact_products_wide(int P, int Pv, int nh, con
                                                       float gamma0, const float* g, const float* gp, float* a_out,
                                                       float* b_out, float* scratch, int& buf) {
   constexpr int BLOCK = kWave * NW;
-  constexpr int E = GT <= 2 ? 2 : DAVA_GV_ENTRIES;
+  constexpr int E = GT <= 2 ? 2 : kGvEntries;
   const int tid = threadIdx.x;
   const int G = (P + 3) / 4;
   const f4v z = f4v{0, 0, 0, 0};
@@ -498,28 +442,14 @@ __device__ __forceinline__ void compact_products_wide(int P, int Pv, int nh, con
 // formula as the generic tail), phi'(0)'s partial d.g, and the history append (W row <- H'y,
 // S row <- s) -- instead of four more passes over workspace vectors (C5: the direction phase was
 // 9% of the solve, profiles/r02_phase_cycles_c5.log).  Returns this thread's d.g partial.
-#ifndef DAVA_GV_FUSED_TAIL
-#define DAVA_GV_FUSED_TAIL 1
-#endif
 // Per entry the four dots are packed 2-wide FMA chains over this thread's groups (v_pk_fma_f32,
-// as the LDS-mode pass does, DAVA_PACKED_HISTORY) and the contributions to H'y, H'g packed FMAs:
-// at C5 (GT = 7) ~250 VALU ops per entry and wave instead of ~420.  (Rejected, interleaved A/B,
+// as the LDS-mode pass does) and the contributions to H'y, H'g packed FMAs: at C5 (GT = 7) ~250
+// VALU ops per entry and wave instead of ~420.  (Rejected, interleaved A/B,
 // profiles/r03_ab_c5_park_yg_lds.log: parking y and g in the dead LDS gradient / direction slots to
 // free registers for two entries per reduction -- bitwise equal, but the per-entry LDS re-reads and
-// the spills cost 14% with one entry and 19% with two.)
-// HYD (DAVA_HY_FROM_D): only H'g is formed from the history; H'y = H'g - H'g_prev = H'g + d_prev,
-// since the previous direction was d_prev = -H' g_prev (H' = H_{k-1} in both).  Two dots and one
-// accumulation per entry instead of four and two, and y / H'y leave the registers, which holds
-// DAVA_GV_ENTRIES_HYD entries per block reduction instead of one.  Same bytes; different rounding.
-#ifndef DAVA_HY_FROM_D
-#define DAVA_HY_FROM_D 0
-#endif
-#ifndef DAVA_HY_FROM_D_LDS
-#define DAVA_HY_FROM_D_LDS 0  // the same for the LDS-mode fused pass (C1-C3)
-#endif
-#ifndef DAVA_GV_ENTRIES_HYD
-#define DAVA_GV_ENTRIES_HYD 2
-#endif
+// the spills cost 14% with one entry and 19% with two.  Forming only H'g from the history and
+// H'y = H'g + d_prev: two entries per reduction, +0.5..0.9% at C5 but a different rounding that moved
+// a C2 problem 2.1e-5 from the oracle, profiles/r03_ab_hy_from_d.log.)
 template <int GT, int NW>
 __device__ __forceinline__ float wide_direction(int P, int Pv, int nh, const float* __restrict__ S,
                                                 const float* __restrict__ W, float* hrho, float* hc, float gamma0,
@@ -527,9 +457,7 @@ __device__ __forceinline__ float wide_direction(int P, int Pv, int nh, const flo
                                                 float* s_row, float* w_row, float* scratch, int& buf, int entry,
                                                 float* tape_rho, float* tape_c) {
   constexpr int BLOCK = kWave * NW;
-  constexpr bool HYD = DAVA_HY_FROM_D;
-  constexpr int E = HYD ? (GT <= 2 ? 4 : DAVA_GV_ENTRIES_HYD) : (GT <= 2 ? 2 : DAVA_GV_ENTRIES);
-  constexpr int ND = HYD ? 2 : 4;  // dots per entry
+  constexpr int E = GT <= 2 ? 2 : kGvEntries;
   const int tid = threadIdx.x;
   const int G = (P + 3) / 4;
   const f4v z = f4v{0, 0, 0, 0};
@@ -540,142 +468,10 @@ __device__ __forceinline__ float wide_direction(int P, int Pv, int nh, const flo
     y[u] = gg[u] = pa[u] = pb[u] = z;
     if (q < G) {
       gg[u] = *reinterpret_cast<const f4v*>(g + 4 * q);
-      if constexpr (!HYD) y[u] = gg[u] - *reinterpret_cast<const f4v*>(gp + 4 * q);
+      y[u] = gg[u] - *reinterpret_cast<const f4v*>(gp + 4 * q);
     }
   }
-  if constexpr (HYD) {
-    for (int j = 0; j < nh; j += E) {
-      const int ne = min(E, nh - j);  // uniform
-      f4v s4[E][GT], w4[E][GT];
-      float dd[ND * E];
-#pragma unroll
-      for (int e = 0; e < E; ++e) {
-#pragma unroll
-        for (int u = 0; u < GT; ++u) {
-          const int q = tid + u * BLOCK;
-          s4[e][u] = w4[e][u] = z;
-          if (e < ne && q < G) {
-            s4[e][u] = *reinterpret_cast<const f4v*>(S + (size_t)(j + e) * Pv + 4 * q);
-            w4[e][u] = *reinterpret_cast<const f4v*>(W + (size_t)(j + e) * Pv + 4 * q);
-          }
-        }
-      }
-#pragma unroll
-      for (int e = 0; e < E; ++e) {
-        f2v sg2 = {0.f, 0.f}, wg2 = {0.f, 0.f};
-#pragma unroll
-        for (int u = 0; u < GT; ++u) {
-          sg2 = pk_fma(s4[e][u].lo, gg[u].lo, sg2); sg2 = pk_fma(s4[e][u].hi, gg[u].hi, sg2);
-          wg2 = pk_fma(w4[e][u].lo, gg[u].lo, wg2); wg2 = pk_fma(w4[e][u].hi, gg[u].hi, wg2);
-        }
-        dd[ND * e] = sg2.x + sg2.y;
-        dd[ND * e + 1] = wg2.x + wg2.y;
-      }
-      block_sum<ND * E, NW>(dd, scratch, buf);
-      buf ^= 1;
-#pragma unroll
-      for (int e = 0; e < E; ++e) {
-        if (e < ne) {
-          const float rho = hrho[j + e], cr = hc[j + e] * rho;
-          const float ag = fmaf(cr, dd[ND * e], -(rho * dd[ND * e + 1])), bg = -rho * dd[ND * e];
-#pragma unroll
-          for (int u = 0; u < GT; ++u) pb[u] = pk_fma4(bg, w4[e][u], pk_fma4(ag, s4[e][u], pb[u]));
-        }
-      }
-    }
-    // H'g = sum + gamma0 g;  H'y = H'g + d_prev (d still holds the previous direction);  y = g - g_prev
-#pragma unroll
-    for (int u = 0; u < GT; ++u) {
-      const int q = tid + u * BLOCK;
-      pb[u] += gamma0 * gg[u];
-      if (q < G) {
-        pa[u] = pb[u] + *reinterpret_cast<const f4v*>(d + 4 * q);
-        y[u] = gg[u] - *reinterpret_cast<const f4v*>(gp + 4 * q);
-      }
-    }
-  }
-#if DAVA_GV_BUFFER_LOADS
-  if constexpr (!HYD) {
-    // Rows through buffer loads: one descriptor per row with the row's length as its range, so the
-    // absent column groups past P load zeros with no exec-mask branch, and each load's address is a
-    // loop-invariant 32-bit lane offset instead of 64-bit arithmetic per load and entry (~100 fewer
-    // instructions per entry and wave at C5).  Same values, same order as the plain loop below:
-    // bitwise equal, but not a reliable gain: interleaved A/B on three boxes, C5 +1.8% on one and
-    // -2.5% on two (problems/s, profiles/r03_ab_buffer_loads.log) -- the GV kernel's register allocation (at
-    // the 256-VGPR cap, ~90 spilled) moves with any change.  Rejected outright: requesting the next
-    // entry's rows before this entry's reduction (all of them, or the S row only) -- the second set
-    // of rows spills inside the loop, C5 -40..-45%.
-    const float* Su = uniform_ptr(S);
-    const float* Wu = uniform_ptr(W);
-    const int row_bytes = 4 * Pv;
-    int voff[GT];
-#pragma unroll
-    for (int u = 0; u < GT; ++u) voff[u] = 16 * (tid + u * BLOCK);
-    auto load_group = [&](int j, f4v (&s4)[E][GT], f4v (&w4)[E][GT]) {
-#pragma unroll
-      for (int e = 0; e < E; ++e) {
-        const int nb = j + e < nh ? row_bytes : 0;  // uniform: an absent entry reads zeros
-        const auto rs = make_rsrc(Su + (size_t)(j + e) * Pv, nb);
-        const auto rw = make_rsrc(Wu + (size_t)(j + e) * Pv, nb);
-#pragma unroll
-        for (int u = 0; u < GT; ++u) {
-          s4[e][u] = buf_ld4(rs, voff[u]);
-          w4[e][u] = buf_ld4(rw, voff[u]);
-        }
-      }
-    };
-    auto dots = [&](const f4v (&s4)[E][GT], const f4v (&w4)[E][GT], float (&dd)[4 * E]) {
-#pragma unroll
-      for (int e = 0; e < E; ++e) {
-        f2v sy2 = {0.f, 0.f}, wy2 = {0.f, 0.f}, sg2 = {0.f, 0.f}, wg2 = {0.f, 0.f};
-#pragma unroll
-        for (int u = 0; u < GT; ++u) {
-          sy2 = pk_fma(s4[e][u].lo, y[u].lo, sy2); sy2 = pk_fma(s4[e][u].hi, y[u].hi, sy2);
-          wy2 = pk_fma(w4[e][u].lo, y[u].lo, wy2); wy2 = pk_fma(w4[e][u].hi, y[u].hi, wy2);
-          sg2 = pk_fma(s4[e][u].lo, gg[u].lo, sg2); sg2 = pk_fma(s4[e][u].hi, gg[u].hi, sg2);
-          wg2 = pk_fma(w4[e][u].lo, gg[u].lo, wg2); wg2 = pk_fma(w4[e][u].hi, gg[u].hi, wg2);
-        }
-        dd[4 * e] = sy2.x + sy2.y;
-        dd[4 * e + 1] = wy2.x + wy2.y;
-        dd[4 * e + 2] = sg2.x + sg2.y;
-        dd[4 * e + 3] = wg2.x + wg2.y;
-      }
-    };
-    auto accumulate = [&](int j, const f4v (&s4)[E][GT], const f4v (&w4)[E][GT], const float (&dd)[4 * E],
-                          const float (&rh)[E], const float (&ch)[E]) {
-#pragma unroll
-      for (int e = 0; e < E; ++e) {
-        if (j + e < nh) {
-          const float rho = rh[e], cr = ch[e] * rho;
-          const float ay = fmaf(cr, dd[4 * e], -(rho * dd[4 * e + 1])), by = -rho * dd[4 * e];
-          const float ag = fmaf(cr, dd[4 * e + 2], -(rho * dd[4 * e + 3])), bg = -rho * dd[4 * e + 2];
-#pragma unroll
-          for (int u = 0; u < GT; ++u) {
-            pa[u] = pk_fma4(by, w4[e][u], pk_fma4(ay, s4[e][u], pa[u]));
-            pb[u] = pk_fma4(bg, w4[e][u], pk_fma4(ag, s4[e][u], pb[u]));
-          }
-        }
-      }
-    };
-    for (int j = 0; j < nh; j += E) {
-      f4v sA[E][GT], wA[E][GT];
-      float dd[4 * E], rh[E], ch[E];
-      load_group(j, sA, wA);
-      dots(sA, wA, dd);
-#pragma unroll
-      for (int e = 0; e < E; ++e) {
-        rh[e] = hrho[min(j + e, nh - 1)];
-        ch[e] = hc[min(j + e, nh - 1)];
-      }
-      block_sum<4 * E, NW>(dd, scratch, buf);
-      buf ^= 1;
-      accumulate(j, sA, wA, dd, rh, ch);
-    }
-  }
-  for (int j = 0; j < 0; j += E) {
-#else
-  for (int j = 0; j < (HYD ? 0 : nh); j += E) {
-#endif
+  for (int j = 0; j < nh; j += E) {
     const int ne = min(E, nh - j);  // uniform
     f4v s4[E][GT], w4[E][GT];
     float dd[4 * E];
@@ -693,7 +489,6 @@ __device__ __forceinline__ float wide_direction(int P, int Pv, int nh, const flo
     }
 #pragma unroll
     for (int e = 0; e < E; ++e) {
-#if DAVA_PACKED_HISTORY
       f2v sy2 = {0.f, 0.f}, wy2 = {0.f, 0.f}, sg2 = {0.f, 0.f}, wg2 = {0.f, 0.f};
 #pragma unroll
       for (int u = 0; u < GT; ++u) {
@@ -706,17 +501,6 @@ __device__ __forceinline__ float wide_direction(int P, int Pv, int nh, const flo
       dd[4 * e + 1] = wy2.x + wy2.y;
       dd[4 * e + 2] = sg2.x + sg2.y;
       dd[4 * e + 3] = wg2.x + wg2.y;
-#else
-      auto dot4 = [](f4v a, f4v b) { const f4v t = a * b; return (t[0] + t[1]) + (t[2] + t[3]); };
-      dd[4 * e] = dd[4 * e + 1] = dd[4 * e + 2] = dd[4 * e + 3] = 0.0f;
-#pragma unroll
-      for (int u = 0; u < GT; ++u) {
-        dd[4 * e] += dot4(s4[e][u], y[u]);
-        dd[4 * e + 1] += dot4(w4[e][u], y[u]);
-        dd[4 * e + 2] += dot4(s4[e][u], gg[u]);
-        dd[4 * e + 3] += dot4(w4[e][u], gg[u]);
-      }
-#endif
     }
     block_sum<4 * E, NW>(dd, scratch, buf);
     buf ^= 1;
@@ -724,7 +508,6 @@ __device__ __forceinline__ float wide_direction(int P, int Pv, int nh, const flo
     for (int e = 0; e < E; ++e) {
       if (e < ne) {
         const float rho = hrho[j + e], cr = hc[j + e] * rho;
-#if DAVA_PACKED_HISTORY
         const float ay = fmaf(cr, dd[4 * e], -(rho * dd[4 * e + 1])), by = -rho * dd[4 * e];
         const float ag = fmaf(cr, dd[4 * e + 2], -(rho * dd[4 * e + 3])), bg = -rho * dd[4 * e + 2];
 #pragma unroll
@@ -732,15 +515,6 @@ __device__ __forceinline__ float wide_direction(int P, int Pv, int nh, const flo
           pa[u] = pk_fma4(by, w4[e][u], pk_fma4(ay, s4[e][u], pa[u]));
           pb[u] = pk_fma4(bg, w4[e][u], pk_fma4(ag, s4[e][u], pb[u]));
         }
-#else
-        const float ay = cr * dd[4 * e] - rho * dd[4 * e + 1], by = -rho * dd[4 * e];
-        const float ag = cr * dd[4 * e + 2] - rho * dd[4 * e + 3], bg = -rho * dd[4 * e + 2];
-#pragma unroll
-        for (int u = 0; u < GT; ++u) {
-          pa[u] += ay * s4[e][u] + by * w4[e][u];
-          pb[u] += ag * s4[e][u] + bg * w4[e][u];
-        }
-#endif
       }
     }
   }
@@ -751,10 +525,8 @@ __device__ __forceinline__ float wide_direction(int P, int Pv, int nh, const flo
   for (int u = 0; u < GT; ++u) {
     const int q = tid + u * BLOCK;
     const f4v yu = y[u], gu = gg[u];
-    if constexpr (!HYD) {
-      pa[u] += gamma0 * yu;
-      pb[u] += gamma0 * gu;
-    }
+    pa[u] += gamma0 * yu;
+    pb[u] += gamma0 * gu;
     sv[u] = q < G ? *reinterpret_cast<const f4v*>(s_cur + 4 * q) : z;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
@@ -812,53 +584,31 @@ __device__ __forceinline__ float wide_direction(int P, int Pv, int nh, const flo
 // latency-bound, few VALU ops per byte) drops to 0 so the partner's objective evaluation or
 // line-search step (VALU/LDS-latency-bound, the critical path) issues first: C3 +1.0%
 // (interleaved A/B, profiles/r01c_ab_wave_priority.log; levels 1..3 within noise of
-// each other).  Equal values = never set.
-#ifndef DAVA_BASE_PRIO
-#define DAVA_BASE_PRIO 2
-#endif
-#ifndef DAVA_HIST_PRIO
-#define DAVA_HIST_PRIO 0
-#endif
-#ifndef DAVA_DEFER_COMBINE
-#define DAVA_DEFER_COMBINE 1
-#endif
+// each other).
+constexpr int kBasePrio = 2;
+constexpr int kHistPrio = 0;
 // EF: history entries in flight per wave (each holds 2 GM float4 rows in registers).  More
 // entries in flight = more bytes outstanding per wave, which is what the history stream of a
-// problem with few waves (or few problems per CU) is bound by.
-#ifndef DAVA_FUSED_INFLIGHT_SMALL
-// (interleaved A/B, profiles/r02_ab_entries_in_flight.log: small 3 / 5 and large 3 are all slower
-// or within noise -- large 3 costs C3 8 %)
-#define DAVA_FUSED_INFLIGHT_SMALL 4  // rows of <= 2 float4 groups per lane (P <= 512)
-#endif
-#ifndef DAVA_FUSED_INFLIGHT_LARGE
-#define DAVA_FUSED_INFLIGHT_LARGE 2  // 3-4 groups per lane (P <= 1024; C3)
-#endif
-// LDS-DMA staging (rejected, r03): EF register entries plus 1-3 more per wave copied HBM -> LDS by
-// global_load_lds_dwordx4 (no VGPRs) in the same batch, in the LDS the resident entries use --
-// bitwise equal, but C2 -2..-5% and C1 (B = 8192) -3..-5%: the resident entries are worth more
-// than the deeper batch (profiles/r03_ab_c2_lds_dma_staging.log).
-// Ring (1): refill each entry slot as soon as it is consumed, so loads overlap the batch's
-// arithmetic.  Rejected: the kernel is at the 256-VGPR cap, the refills keep the slots live
-// through every consume, and the spills (scratch ops 26 -> 201) cost C3 -33 %, C2 -13 %
-// (interleaved A/B, bitwise equal, profiles/r02_ab_history_ring.log).
-#ifndef DAVA_HISTORY_RING
-#define DAVA_HISTORY_RING 0  // 0: load a batch of EF entries, consume it, then load the next
-#endif
+// problem with few waves (or few problems per CU) is bound by.  (Interleaved A/B,
+// profiles/r02_ab_entries_in_flight.log: 3 / 5 for short rows and 3 for long rows are slower or
+// within noise -- 3 costs C3 8%.)
+// Rejected, r03: LDS-DMA staging of 1-3 more entries per wave by global_load_lds_dwordx4 (no VGPRs),
+// in the LDS the resident entries use -- bitwise equal, but C2 -2..-5% and C1 (B = 8192) -3..-5%
+// (profiles/r03_ab_c2_lds_dma_staging.log).  Rejected, r02: refilling each entry slot as soon as it
+// is consumed (a register ring) -- at the 256-VGPR cap the spills (scratch ops 26 -> 201) cost C3 33%,
+// C2 13% (profiles/r02_ab_history_ring.log).
 template <int GM>
 __host__ __device__ constexpr int fused_inflight() {
-  return DAVA_FUSED_PAIR ? (GM <= 2 ? DAVA_FUSED_INFLIGHT_SMALL : DAVA_FUSED_INFLIGHT_LARGE) : 1;
+  return GM <= 2 ? 4 : 2;  // rows of <= 2 float4 groups per lane (P <= 512: C1, C2) : 3-4 groups (C3)
 }
 template <int GM, int NW>
 __device__ __forceinline__ void compact_products_fused(int P, int Pv, int nh, const float* __restrict__ S,
                                        const float* __restrict__ W, const float* LH, int lcap,
                                        const float* hrho, const float* hc,
                                        float gamma0, const float* g, const float* gp, float* a_out, float* b_out,
-                                       float* spare0, float* spare1, float* spare2, float* spare3,
-                                       const float* dprev) {
+                                       float* spare0, float* spare1, float* spare2, float* spare3) {
   static_assert(NW == 1 || NW == 2 || NW == 4, "the cross-wave combine is written for 1, 2 or 4 waves");
   constexpr int EF = fused_inflight<GM>();
-  constexpr bool HYD = DAVA_HY_FROM_D_LDS;
-  static_assert(!HYD || NW == 1 || DAVA_DEFER_COMBINE, "H'y from d: the deferred cross-wave combine");
   const int lane = threadIdx.x & (kWave - 1);
   const int wave = threadIdx.x / kWave;
   const int G = (P + 3) / 4;
@@ -884,44 +634,7 @@ __device__ __forceinline__ void compact_products_fused(int P, int Pv, int nh, co
   // one transposed wave reduction of the four (wave_sum4: uniform results), then the entry's
   // contribution to H y and H g as packed FMAs.  ~90 VALU ops per entry at GM = 4 (the round-1
   // form, per-element products + one wave_sum per dot: ~210).
-  // HYD (DAVA_HY_FROM_D_LDS): only H'g is formed from the history -- two dots (s.g, w.g) and one
-  // accumulation per entry; H'y = H'g + d_prev after the pass (d_prev = -H' g_prev, the same H').
-  // Two entries share one transposed wave reduction (consume_pair).
-  auto acc_g = [&](int j, float sg, float wg, const f4v (&s4)[GM], const f4v (&w4)[GM]) {
-    const float rho = hrho[j], cr = hc[j] * rho;
-    const float ag = fmaf(cr, sg, -(rho * wg)), bg = -rho * sg;
-#pragma unroll
-    for (int m = 0; m < GM; ++m) pb[m] = pk_fma4(bg, w4[m], pk_fma4(ag, s4[m], pb[m]));
-  };
-  auto gdots = [&](const f4v (&s4)[GM], const f4v (&w4)[GM], float& sg, float& wg) {
-    f2v sg2 = {0.f, 0.f}, wg2 = {0.f, 0.f};
-#pragma unroll
-    for (int m = 0; m < GM; ++m) {
-      const f4v gm = gvec(m);
-      sg2 = pk_fma(s4[m].lo, gm.lo, sg2); sg2 = pk_fma(s4[m].hi, gm.hi, sg2);
-      wg2 = pk_fma(w4[m].lo, gm.lo, wg2); wg2 = pk_fma(w4[m].hi, gm.hi, wg2);
-    }
-    sg = sg2.x + sg2.y;
-    wg = wg2.x + wg2.y;
-  };
-  auto consume_pair = [&](int j0, const f4v (&s0)[GM], const f4v (&w0)[GM], int j1, const f4v (&s1)[GM],
-                          const f4v (&w1)[GM]) {
-    float a0, b0, a1, b1;
-    gdots(s0, w0, a0, b0);
-    gdots(s1, w1, a1, b1);
-    const float4 t = wave_sum4(a0, b0, a1, b1);
-    acc_g(j0, t.x, t.y, s0, w0);
-    acc_g(j1, t.z, t.w, s1, w1);
-  };
   auto consume = [&](int j, const f4v (&s4)[GM], const f4v (&w4)[GM]) {
-    if constexpr (HYD) {
-      float a0, b0;
-      gdots(s4, w4, a0, b0);
-      const float4 t = wave_sum4(a0, b0, 0.f, 0.f);
-      acc_g(j, t.x, t.y, s4, w4);
-      return;
-    }
-#if DAVA_PACKED_HISTORY
     f2v sy2 = {0.f, 0.f}, wy2 = {0.f, 0.f}, sg2 = {0.f, 0.f}, wg2 = {0.f, 0.f};
 #pragma unroll
     for (int m = 0; m < GM; ++m) {
@@ -933,19 +646,6 @@ __device__ __forceinline__ void compact_products_fused(int P, int Pv, int nh, co
     }
     const float4 t = wave_sum4(sy2.x + sy2.y, wy2.x + wy2.y, sg2.x + sg2.y, wg2.x + wg2.y);
     const float sy = t.x, wy = t.y, sg = t.z, wg = t.w;
-#else
-    float sy = 0.f, wy = 0.f, sg = 0.f, wg = 0.f;
-#pragma unroll
-    for (int m = 0; m < GM; ++m) {
-      const f4v y = yvec(m), gm = gvec(m);
-      const f4v a = s4[m] * y, b = w4[m] * y, c = s4[m] * gm, e = w4[m] * gm;
-      sy += (a[0] + a[1]) + (a[2] + a[3]);
-      wy += (b[0] + b[1]) + (b[2] + b[3]);
-      sg += (c[0] + c[1]) + (c[2] + c[3]);
-      wg += (e[0] + e[1]) + (e[2] + e[3]);
-    }
-    sy = wave_sum(sy); wy = wave_sum(wy); sg = wave_sum(sg); wg = wave_sum(wg);
-#endif
     // coefficients with the FMA written out: both call sites (LDS- and HBM-resident entries) must
     // round them identically, and left to itself the compiler contracted cr sy - rho wy into an
     // FMA at one site and not the other (hip's __fmul_rn / __fsub_rn do not stop contraction)
@@ -954,19 +654,14 @@ __device__ __forceinline__ void compact_products_fused(int P, int Pv, int nh, co
     const float ag = fmaf(cr, sg, -(rho * wg)), bg = -rho * sg;
 #pragma unroll
     for (int m = 0; m < GM; ++m) {
-#if DAVA_PACKED_HISTORY
       pa[m] = pk_fma4(by, w4[m], pk_fma4(ay, s4[m], pa[m]));
       pb[m] = pk_fma4(bg, w4[m], pk_fma4(ag, s4[m], pb[m]));
-#else
-      pa[m] += ay * s4[m] + by * w4[m];
-      pb[m] += ag * s4[m] + bg * w4[m];
-#endif
     }
   };
-  // buffer loads (rows of <= DAVA_FUSED_BUFFER_LOADS_GM groups per lane): a descriptor per row (range =
+  // buffer loads (rows of <= kFusedBufferLoadsGM groups per lane): a descriptor per row (range =
   // the row), lane offsets loop-invariant, the groups past P read zeros through the range check
   // instead of an exec-mask branch (bitwise equal)
-  constexpr bool kBufferLoads = GM <= DAVA_FUSED_BUFFER_LOADS_GM;
+  constexpr bool kBufferLoads = GM <= kFusedBufferLoadsGM;
   const float* Su = uniform_ptr(S);
   const float* Wu = uniform_ptr(W);
   auto load = [&](int j, f4v (&s4)[GM], f4v (&w4)[GM]) {
@@ -989,9 +684,7 @@ __device__ __forceinline__ void compact_products_fused(int P, int Pv, int nh, co
       }
     }
   };
-#if DAVA_HIST_PRIO != DAVA_BASE_PRIO
-  __builtin_amdgcn_s_setprio(DAVA_HIST_PRIO);
-#endif
+  __builtin_amdgcn_s_setprio(kHistPrio);
   int j = wave;
   for (const int nl = min(lcap, nh); j < nl; j += NW) {  // on-chip entries first (wave-uniform)
     f4v s0[GM], w0[GM];
@@ -1005,51 +698,24 @@ __device__ __forceinline__ void compact_products_fused(int P, int Pv, int nh, co
     }
     consume(j, s0, w0);
   }
-  if constexpr (EF > 1) {  // EF entries of this wave in flight: all loads issued before any is consumed
-#if DAVA_HISTORY_RING
-    // ring: each register slot is refilled with the entry EF * NW ahead as soon as it has been
-    // consumed, so the next entries' loads are in flight while this batch is consumed (the batch
-    // form waits out a full load latency per batch).  Same entries, same order: bitwise equal.
-    if (j + (EF - 1) * NW < nh) {
-      f4v s[EF][GM], w[EF][GM];
+  // EF entries of this wave in flight: all loads issued before any is consumed
+  for (; j + (EF - 1) * NW < nh; j += EF * NW) {
+    f4v s[EF][GM], w[EF][GM];
 #pragma unroll
-      for (int e = 0; e < EF; ++e) load(j + e * NW, s[e], w[e]);
-      for (; j + (2 * EF - 1) * NW < nh; j += EF * NW) {
+    for (int e = 0; e < EF; ++e) load(j + e * NW, s[e], w[e]);
 #pragma unroll
-        for (int e = 0; e < EF; ++e) {
-          consume(j + e * NW, s[e], w[e]);
-          load(j + (EF + e) * NW, s[e], w[e]);
-        }
-      }
-#pragma unroll
-      for (int e = 0; e < EF; ++e) consume(j + e * NW, s[e], w[e]);
-      j += EF * NW;
-    }
-#else
-    for (; j + (EF - 1) * NW < nh; j += EF * NW) {
-      f4v s[EF][GM], w[EF][GM];
-#pragma unroll
-      for (int e = 0; e < EF; ++e) load(j + e * NW, s[e], w[e]);
-      if constexpr (HYD && EF % 2 == 0) {
-#pragma unroll
-        for (int e = 0; e < EF; e += 2) consume_pair(j + e * NW, s[e], w[e], j + (e + 1) * NW, s[e + 1], w[e + 1]);
-      } else {
-#pragma unroll
-        for (int e = 0; e < EF; ++e) consume(j + e * NW, s[e], w[e]);
-      }
-    }
-#endif
+    for (int e = 0; e < EF; ++e) consume(j + e * NW, s[e], w[e]);
   }
   for (; j < nh; j += NW) {  // the rest, one entry in flight
     f4v s0[GM], w0[GM];
     load(j, s0, w0);
     consume(j, s0, w0);
   }
-#if DAVA_HIST_PRIO != DAVA_BASE_PRIO
-  __builtin_amdgcn_s_setprio(DAVA_BASE_PRIO);
-#endif
+  __builtin_amdgcn_s_setprio(kBasePrio);
   // deterministic cross-wave sum: ((w0 + w2) + (w1 + w3)) + gamma0 * (y | g)  (NW = 4),
-  // (w0 + w1) + gamma0 * (y | g)  (NW = 2), w0 + gamma0 * (y | g)  (NW = 1)
+  // (w0 + w1) + gamma0 * (y | g)  (NW = 2), w0 + gamma0 * (y | g)  (NW = 1).  With NW > 1 the last
+  // adds are left to the caller's block-wide pass after its barrier (same operations, same order):
+  // (w0 + w2) | w0 in spare0/1 and (w1 + w3) | w1 in spare2/3.
   auto put = [&](float* A, float* B) {
 #pragma unroll
     for (int m = 0; m < GM; ++m)
@@ -1068,81 +734,26 @@ __device__ __forceinline__ void compact_products_fused(int P, int Pv, int nh, co
         pb[m] += *reinterpret_cast<const f4v*>(B + 4 * q);
       }
   };
-  auto finish = [&]() {  // + gamma0 (y | g), into the outputs
+  if constexpr (NW == 1) {  // + gamma0 (y | g), into the outputs
 #pragma unroll
     for (int m = 0; m < GM; ++m)
       if (ok[m]) {
-        if constexpr (HYD) {
-          pb[m] += gamma0 * gvec(m);
-          pa[m] = pb[m] + *reinterpret_cast<const f4v*>(dprev + 4 * (lane + kWave * m));
-        } else {
-          pa[m] += gamma0 * yvec(m);
-          pb[m] += gamma0 * gvec(m);
-        }
+        pa[m] += gamma0 * yvec(m);
+        pb[m] += gamma0 * gvec(m);
       }
     put(a_out, b_out);
-  };
-  if constexpr (NW == 1) {
-    finish();
-    return;
-  }
-  if constexpr (HYD) {
-    // only H'g partials: w0 (+ w2) into spare0, w1 (+ w3) into spare1; the caller's block-wide
-    // pass adds them, gamma0 g and d_prev (spare2 / spare3 and d stay untouched)
-    auto put1 = [&](float* B) {
-#pragma unroll
-      for (int m = 0; m < GM; ++m)
-        if (ok[m]) *reinterpret_cast<f4v*>(B + 4 * (lane + kWave * m)) = pb[m];
-    };
-    auto add1 = [&](const float* B) {
-#pragma unroll
-      for (int m = 0; m < GM; ++m)
-        if (ok[m]) pb[m] += *reinterpret_cast<const f4v*>(B + 4 * (lane + kWave * m));
-    };
-    if constexpr (NW == 2) {
-      put1(wave == 0 ? spare0 : spare1);
-      return;
-    }
-    if (wave == 2) put1(spare0);
-    if (wave == 3) put1(spare1);
-    __syncthreads();
-    if (wave == 0) { add1(spare0); put1(spare0); }
-    if (wave == 1) { add1(spare1); put1(spare1); }
     return;
   }
   if constexpr (NW == 2) {
-    // deferred: w0 in spare0/1, w1 in spare2/3; the caller's block-wide pass adds them and
-    // gamma0 (y | g) element by element after its barrier (same operations, same order)
-    if (DAVA_DEFER_COMBINE) {
-      if (wave == 0) put(spare0, spare1);
-      if (wave == 1) put(spare2, spare3);
-      return;
-    }
-    if (wave == 1) put(spare0, spare1);
-    __syncthreads();
-    if (wave == 0) {
-      add(spare0, spare1);
-      finish();
-    }
+    if (wave == 0) put(spare0, spare1);
+    if (wave == 1) put(spare2, spare3);
     return;
   }
   if (wave == 2) put(spare0, spare1);
   if (wave == 3) put(spare2, spare3);
   __syncthreads();
-  if (DAVA_DEFER_COMBINE) {
-    // leave (w0 + w2) in spare0/1 and (w1 + w3) in spare2/3: the caller's block-wide pass
-    // adds them and gamma0 (y | g) element by element (same operations, same order)
-    if (wave == 0) { add(spare0, spare1); put(spare0, spare1); }
-    if (wave == 1) { add(spare2, spare3); put(spare2, spare3); }
-    return;
-  }
-  if (wave == 0) add(spare0, spare1);
+  if (wave == 0) { add(spare0, spare1); put(spare0, spare1); }
   if (wave == 1) { add(spare2, spare3); put(spare2, spare3); }
-  __syncthreads();
-  if (wave == 0) {
-    add(spare2, spare3);
-    finish();
-  }
 }
 
 // XL: GV mode with x, d and the objective's gradient in LDS.  PPT > 0: the objective keeps
@@ -1150,15 +761,13 @@ __device__ __forceinline__ void compact_products_fused(int P, int Pv, int nh, co
 // NW: waves per workgroup -- 8 in GV mode; 4 (default) or 2 in LDS mode (two-wave workgroups put
 // twice as many small problems on a CU at once, DESIGN.md 3.1 Launch).
 template <int MODE, bool GV, int RES, bool XL, int PPT, int NW>
-__global__ __launch_bounds__(kWave * NW, DAVA_SOLVE_WAVES_PER_EU) void bfgs_ba_solve_kernel(SolveArgs a) {
+__global__ __launch_bounds__(kWave * NW, kSolveWavesPerEU) void bfgs_ba_solve_kernel(SolveArgs a) {
   static_assert(!XL || GV, "XL is a global-vector-mode variant");
   static_assert(GV ? NW == solve_waves(true) : (NW == 1 || NW == 2 || NW == 4), "LDS mode runs 1-, 2- or 4-wave workgroups");
   constexpr int BLOCK = kWave * NW;
-  constexpr bool kTrialDot = GV ? DAVA_TRIAL_DOT_GV : DAVA_TRIAL_DOT;
+  constexpr bool kTrialDot = GV ? kTrialDotGv : kTrialDotLds;
   extern __shared__ __attribute__((aligned(16))) float lds[];
-#if DAVA_BASE_PRIO
-  __builtin_amdgcn_s_setprio(DAVA_BASE_PRIO);
-#endif
+  __builtin_amdgcn_s_setprio(kBasePrio);
   const Layout L = a.L;
   const int P = L.P, M = L.M, N = L.N;
   const int Pv = a.Pv;
@@ -1284,7 +893,7 @@ __global__ __launch_bounds__(kWave * NW, DAVA_SOLVE_WAVES_PER_EU) void bfgs_ba_s
       if (have_next) {
         E = E_next;
       } else {
-        ba_eval<true, false, false, false, false, RES, float, NW, PPT, GV && DAVA_PACKED_PAIRS>(L, x, nullptr, 0.f, obs, vis, grad_buf(g), views, vpart,
+        ba_eval<true, false, false, false, false, RES, float, NW, PPT, GV>(L, x, nullptr, 0.f, obs, vis, grad_buf(g), views, vpart,
                                                                   scratch, buf, E, unused);
         publish(g);
         ++evals;
@@ -1332,17 +941,13 @@ __global__ __launch_bounds__(kWave * NW, DAVA_SOLVE_WAVES_PER_EU) void bfgs_ba_s
           }
           // (no barrier needed: each thread reads back only its own hy_new / hg below)
         } else {
-  #if DAVA_DIAG_NO_SWEEP  // timing-only build: H stays gamma0 I (results are wrong)
-          for (int i = tid; i < P; i += BLOCK) { hy_new[i] = gamma0 * (g[i] - gp[i]); hg[i] = gamma0 * g[i]; }
-  #else
           if constexpr (MODE == DAVA_HESSIAN_DENSE) {
             dense_sweep<NW>(L, a.Pld, H, materialized, gamma0, s_pend, hy_pend, pend_rho, pend_c, g, gp, hy_new, hg);
             materialized = true;
           } else {
-  #ifndef DAVA_COMPACT_TWO_PASS
             const int G4 = (P + 3) / 4;
             const int GM = (G4 + kWave - 1) / kWave;
-            deferred = DAVA_DEFER_COMBINE && !GV && NW > 1 && GM <= 4;
+            deferred = !GV && NW > 1 && GM <= 4;
             if constexpr (GV) {  // workgroup-wide single pass, else two passes
               const int GT = (G4 + kWave * NW - 1) / (kWave * NW);
               const int nh = k - 1;
@@ -1350,7 +955,7 @@ __global__ __launch_bounds__(kWave * NW, DAVA_SOLVE_WAVES_PER_EU) void bfgs_ba_s
               float* tcp = tr ? tr + a.iters : nullptr;
               float* srow = SH + (size_t)(k - 1) * Pv;
               float* wrow = WH + (size_t)(k - 1) * Pv;
-              const bool fuse = DAVA_GV_FUSED_TAIL && wide_history_pass(Pv, a.kcap, GV) && k - 1 < a.kcap;
+              const bool fuse = wide_history_pass(Pv, a.kcap, GV) && k - 1 < a.kcap;
               if (fuse) {
                 tail_done = true;
                 if (GT <= 1) dg = wide_direction<1, NW>(P, Pv, nh, SH, WH, hrho, hc, gamma0, g, gp, s_cur, d, srow, wrow, scratch, buf, k - 1, tr, tcp);
@@ -1370,17 +975,15 @@ __global__ __launch_bounds__(kWave * NW, DAVA_SOLVE_WAVES_PER_EU) void bfgs_ba_s
               else if (GT == 6) compact_products_wide<6, NW>(P, Pv, nh, SH, WH, hrho, hc, gamma0, g, gp, hy_new, hg, scratch, buf);
               else compact_products_wide<7, NW>(P, Pv, nh, SH, WH, hrho, hc, gamma0, g, gp, hy_new, hg, scratch, buf);
             } else
-            if (GM <= 1) compact_products_fused<1, NW>(P, Pv, k - 1, SH, WH, LH, lcap, hrho, hc, gamma0, g, gp, hy_new, hg, s_pend, hy_pend, d, hg, d);
-            else if (GM == 2) compact_products_fused<2, NW>(P, Pv, k - 1, SH, WH, LH, lcap, hrho, hc, gamma0, g, gp, hy_new, hg, s_pend, hy_pend, d, hg, d);
-            else if (GM == 3) compact_products_fused<3, NW>(P, Pv, k - 1, SH, WH, LH, lcap, hrho, hc, gamma0, g, gp, hy_new, hg, s_pend, hy_pend, d, hg, d);
-            else if (GM == 4) compact_products_fused<4, NW>(P, Pv, k - 1, SH, WH, LH, lcap, hrho, hc, gamma0, g, gp, hy_new, hg, s_pend, hy_pend, d, hg, d);
+            if (GM <= 1) compact_products_fused<1, NW>(P, Pv, k - 1, SH, WH, LH, lcap, hrho, hc, gamma0, g, gp, hy_new, hg, s_pend, hy_pend, d, hg);
+            else if (GM == 2) compact_products_fused<2, NW>(P, Pv, k - 1, SH, WH, LH, lcap, hrho, hc, gamma0, g, gp, hy_new, hg, s_pend, hy_pend, d, hg);
+            else if (GM == 3) compact_products_fused<3, NW>(P, Pv, k - 1, SH, WH, LH, lcap, hrho, hc, gamma0, g, gp, hy_new, hg, s_pend, hy_pend, d, hg);
+            else if (GM == 4) compact_products_fused<4, NW>(P, Pv, k - 1, SH, WH, LH, lcap, hrho, hc, gamma0, g, gp, hy_new, hg, s_pend, hy_pend, d, hg);
             else
-  #endif
             // GV mode (very long rows, few resident waves): 8 column groups in flight per lane;
             // the LDS-mode kernel keeps the lean loop (its register budget is the fused pass's)
             compact_products<GV ? 8 : 1, NW>(P, Pv, k - 1, SH, WH, hcoef, hrho, hc, gamma0, g, gp, hy_new, hg);
           }
-  #endif
           if (!tail_done) {
           __syncthreads();
           DAVA_PHASE(1);
@@ -1388,16 +991,10 @@ __global__ __launch_bounds__(kWave * NW, DAVA_SOLVE_WAVES_PER_EU) void bfgs_ba_s
             for (int i = tid; i < P; i += BLOCK) {
               const float gi = g[i], yi = gi - gp[i], si = s_cur[i];
               float hi, gh;
-              if constexpr (DAVA_HY_FROM_D_LDS) {  // H'g partials in s_pend / hy_pend; H'y = H'g + d_prev
-                gh = s_pend[i] + hy_pend[i];
-                gh += gamma0 * gi;
-                hi = gh + d[i];
-              } else {
-                hi = s_pend[i] + d[i];
-                gh = hy_pend[i] + hg[i];
-                hi += gamma0 * yi;
-                gh += gamma0 * gi;
-              }
+              hi = s_pend[i] + d[i];
+              gh = hy_pend[i] + hg[i];
+              hi += gamma0 * yi;
+              gh += gamma0 * gi;
               hy_new[i] = hi;
               hg[i] = gh;
               r[0] += si * yi; r[1] += hi * yi; r[2] += si * gi; r[3] += hi * gi;
@@ -1487,14 +1084,13 @@ __global__ __launch_bounds__(kWave * NW, DAVA_SOLVE_WAVES_PER_EU) void bfgs_ba_s
         // phi'(0).  The check rides on the objective's first reduction (CHECK).  Otherwise
         // E and the full gradient at the trial point are formed (kept for reuse as the
         // next iterate's gradient) and phi'(alpha) = d . grad (DOT).
-        const bool known_same = DAVA_TRIAL_CHECK && al <= nomove_al;  // uniform
+        const bool known_same = al <= nomove_al;  // uniform
         if (!known_same &&
-            ba_eval<true, !kTrialDot, true, kTrialDot, DAVA_TRIAL_CHECK, RES, float, NW, PPT,
-                    GV && DAVA_PACKED_PAIRS>(
+            ba_eval<true, !kTrialDot, true, kTrialDot, true, RES, float, NW, PPT,
+                    GV>(
                 L, x, d, al, obs, vis, grad_buf(gp), views, vpart, scratch, buf, fa, dfa)) {
           ++evals;
           last_same = false;
-#if DAVA_NONFINITE_DOT
           // Overflowed trial (fp32 at a wild step): the reference's phi'(alpha) is autograd w.r.t.
           // alpha, i.e. (grad E(x + alpha d) * d).sum() (wolfe_conditions.py:134-143) -- NaN as
           // soon as the reverse-mode gradient holds a NaN or infinities of both signs, where the
@@ -1510,7 +1106,6 @@ __global__ __launch_bounds__(kWave * NW, DAVA_SOLVE_WAVES_PER_EU) void bfgs_ba_s
             block_sum<1, NW>(r, scratch, buf); buf ^= 1;
             dfa = r[0];
           }
-#endif
         } else {
           fa = E;
           dfa = dphi0;
@@ -1518,12 +1113,6 @@ __global__ __launch_bounds__(kWave * NW, DAVA_SOLVE_WAVES_PER_EU) void bfgs_ba_s
           if (!known_same) nomove_al = al;
         }
         DAVA_PHASE(3);
-#if DAVA_DEBUG_TRIALS >= 0
-        // diagnostic builds only (make variant FLAGS=-DDAVA_DEBUG_TRIALS=<problem>): every trial
-        if (b == DAVA_DEBUG_TRIALS && tid == 0)
-          printf("TRIAL k=%d t=%d alpha=%.9g f=%.9g dphi=%.9g f0=%.9g dphi0=%.9g lo=%.9g hi=%.9g zoom=%d\n", k, t, al,
-                 fa, dfa, E, dphi0, a_lo, a_hi, (int)zoom);
-#endif
         ++trials;
         evaluated = true;
         last_al = al;
@@ -1604,7 +1193,7 @@ __global__ __launch_bounds__(kWave * NW, DAVA_SOLVE_WAVES_PER_EU) void bfgs_ba_s
     for (int i = tid; i < P; i += BLOCK) xo[i] = x[i];
     if (a.err_out) {
       float e2 = 0.f;
-      ba_eval<false, false, false, false, false, RES, float, NW, PPT, GV && DAVA_PACKED_PAIRS>(L, x, nullptr, 0.f, obs, vis, nullptr, views, vpart, scratch, buf,
+      ba_eval<false, false, false, false, false, RES, float, NW, PPT, GV>(L, x, nullptr, 0.f, obs, vis, nullptr, views, vpart, scratch, buf,
                                                      e2, unused);
       if (tid == 0) a.err_out[b] = e2;
     }
@@ -1697,13 +1286,9 @@ static size_t dense_hessian_bytes(const DavaScene* s) {
   return (size_t)s->batch * (size_t)P * (size_t)round_up(P, 32) * sizeof(float);
 }
 
-#ifndef DAVA_EXTRA_LDS
-#define DAVA_EXTRA_LDS 0  // diagnostic builds only: pad LDS to force fewer workgroups per CU
-#endif
 static int lds_bytes_for(const DavaScene* s, int kcap = 0, bool gv = false, int lcap = 0, bool xl = false,
                          int nw = 0) {
-  return carve_lds(s->num_views, s->num_points, round_up(s->num_parameters, 4), kcap, gv, lcap, xl, nw).total_bytes +
-         DAVA_EXTRA_LDS;
+  return carve_lds(s->num_views, s->num_points, round_up(s->num_parameters, 4), kcap, gv, lcap, xl, nw).total_bytes;
 }
 
 // Waves per LDS-mode workgroup (GV mode: always 8).  The register budget (256 VGPRs) holds two
@@ -1713,12 +1298,11 @@ static int lds_bytes_for(const DavaScene* s, int kcap = 0, bool gv = false, int 
 // (interleaved A/B, profiles/r02_ab_waves.log: C2 +19%, 8192 two-view 64-point problems +49%,
 // C3 -17% at two).  One wave per problem measured another +9% on the 64-point shape but put one
 // K = 100 run-to-stagnation problem 3e-5 from the oracle (30x the reference's own 1-ulp
-// sensitivity), so it stays opt-in.  DENSE keeps 4.  DAVA_SOLVE_WAVES=1|2|4 overrides (A/B, tests).
+// sensitivity), so it stays opt-in.  DENSE keeps 4.  The kDbgSolveWaves override (1 | 2 | 4) is for
+// A/B runs and tests.
 static int lds_mode_waves(const DavaScene* s, int mode) {
-  if (const char* e = getenv("DAVA_SOLVE_WAVES")) {
-    const int w = atoi(e);
-    if (w == 1 || w == 2 || w == 4) return w;
-  }
+  const long long w = debug_knob(kDbgSolveWaves);
+  if (w == 1 || w == 2 || w == 4) return (int)w;
   if (mode != DAVA_HESSIAN_COMPACT) return 4;
   const int groups = (round_up(s->num_parameters, 4) / 4 + kWave - 1) / kWave;  // per-lane float4 groups at 1 wave
   return groups <= 2 ? 2 : 4;
@@ -1732,13 +1316,12 @@ static int solve_waves_for(const DavaScene* s, bool gv, int mode) {
 constexpr int kLdsModeBudget = 72 * 1024;
 constexpr int kMaxLds = 160 * 1024;
 static bool use_gv(const DavaScene* s, int kcap = 0) {
-  const bool force = getenv("DAVA_FORCE_GV") != nullptr;  // test knob: cross-check GV vs LDS mode
-  return force || lds_bytes_for(s, kcap, false) > kLdsModeBudget;
+  return debug_flag(kDbgForceGV) || lds_bytes_for(s, kcap, false) > kLdsModeBudget;
 }
 // GV mode: run the objective on LDS copies of x and d (carve_lds `xl`) whenever they fit
-// beside the rest of the image.  DAVA_GV_NO_XL forces the in-workspace variant (tests).
+// beside the rest of the image.  The kDbgGVNoXL override forces the in-workspace variant (tests).
 static bool use_xl(const DavaScene* s, int kcap, bool gv) {
-  if (!gv || getenv("DAVA_GV_NO_XL") != nullptr) return false;
+  if (!gv || debug_flag(kDbgGVNoXL)) return false;
   return lds_bytes_for(s, kcap, true, 0, true) <= kMaxLds;
 }
 static size_t gv_vector_bytes(const DavaScene* s) {
@@ -1755,21 +1338,18 @@ static size_t compact_history_bytes(const DavaScene* s, const DavaSolverConfig* 
 
 // COMPACT, LDS mode, single-pass products: how many of the oldest history entries to keep
 // on-chip.  Default: whatever fits beside the problem image without lowering the number of
-// workgroups a CU holds at the register limit (4 SIMDs x DAVA_SOLVE_WAVES_PER_EU waves / nw:
-// two 4-wave workgroups of 80 KiB, or four 2-wave workgroups of 40 KiB); DAVA_LDS_HISTORY=n
-// overrides (A/B and tests; 0 = all in HBM; values past one workgroup's LDS are clamped).
+// workgroups a CU holds at the register limit (4 SIMDs x kSolveWavesPerEU waves / nw:
+// two 4-wave workgroups of 80 KiB, or four 2-wave workgroups of 40 KiB); the kDbgLdsHistory override
+// sets the count (A/B and tests; 0 = all in HBM; values past one workgroup's LDS are clamped).
 static int lds_history_entries(const DavaScene* s, int kcap, bool gv, int nw) {
-#ifdef DAVA_COMPACT_TWO_PASS
-  return 0;
-#endif
   const int Pv = round_up(s->num_parameters, 4);
   if (gv || kcap <= 0 || (Pv / 4 + kWave - 1) / kWave > 4) return 0;
   const int base = lds_bytes_for(s, kcap, false, 0, false, nw);
   const int per = 2 * Pv * (int)sizeof(float);
-  int per_cu = 4 * DAVA_SOLVE_WAVES_PER_EU / nw;  // workgroups per CU at the register limit
-  if (const char* e = getenv("DAVA_WG_PER_CU")) per_cu = max(1, atoi(e));  // A/B knob: LDS budget = 160 KB / this
+  int per_cu = 4 * kSolveWavesPerEU / nw;  // workgroups per CU at the register limit
+  if (debug_knob(kDbgWgPerCu) > 0) per_cu = (int)debug_knob(kDbgWgPerCu);  // A/B: LDS budget = 160 KB / this
   int n = (kMaxLds / per_cu - base) / per;
-  if (const char* e = getenv("DAVA_LDS_HISTORY")) n = atoi(e);
+  if (debug_knob(kDbgLdsHistory) >= 0) n = (int)debug_knob(kDbgLdsHistory);
   n = min(n, (kMaxLds - base) / per);
   return max(0, min(n, kcap));
 }
@@ -1777,6 +1357,29 @@ static int lds_history_entries(const DavaScene* s, int kcap, bool gv, int nw) {
 }  // namespace dava
 
 using namespace dava;
+
+// ---- debug overrides (dava_debug.hpp): set only through the two calls below, never from the environment ----
+namespace dava {
+static long long g_debug_knobs[kDbgKnobs] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};
+static const char* const kDebugKnobNames[kDbgKnobs] = {
+    "FORCE_GV", "GV_NO_XL", "SOLVE_WAVES", "WG_PER_CU", "LDS_HISTORY", "STAGGER", "STAGGER_LEVELS",
+    "NO_PPT", "NO_QUEUE", "ADJ_GV_WAVES", "ADJ_FORCE_GV", "ADJ_LDS_ENTRIES", "ADJ_GD_HBM"};
+long long debug_knob(int k) { return k >= 0 && k < kDbgKnobs ? g_debug_knobs[k] : -1; }
+}  // namespace dava
+
+extern "C" int dava_debug_set_override(const char* name, int64_t value) {
+  if (!name) return DAVA_ERR_INVALID_ARGUMENT;
+  for (int k = 0; k < kDbgKnobs; ++k)
+    if (strcmp(name, kDebugKnobNames[k]) == 0) {
+      g_debug_knobs[k] = value < 0 ? -1 : value;
+      return DAVA_OK;
+    }
+  return DAVA_ERR_INVALID_ARGUMENT;
+}
+
+extern "C" void dava_debug_clear_overrides(void) {
+  for (int k = 0; k < kDbgKnobs; ++k) g_debug_knobs[k] = -1;
+}
 
 // Bytes of the solve's state (vectors in GV mode + inverse-Hessian state); the work-queue
 // counter follows at that offset, in the last kQueueBytes of the workspace.
@@ -1833,8 +1436,8 @@ static void launch_solve_ppt(const SolveArgs& a, int B, int lds, hipStream_t s) 
   // stagger only a launch whose problems all run at once (one round, B <= slots)
   args.stagger = slots > 0 && B <= slots && B > 1 ? kStaggerCycles : 0;
   args.stagger_levels = 1;
-  if (const char* e = getenv("DAVA_STAGGER")) args.stagger = max(0, atoi(e));  // A/B knob (cycles)
-  if (const char* e = getenv("DAVA_STAGGER_LEVELS")) args.stagger_levels = max(1, atoi(e));
+  if (debug_knob(kDbgStagger) >= 0) args.stagger = (int)debug_knob(kDbgStagger);  // A/B (cycles)
+  if (debug_knob(kDbgStaggerLevels) >= 1) args.stagger_levels = (int)debug_knob(kDbgStaggerLevels);
   if (args.queue) {  // one workgroup per resident slot
     if (slots > 0) grid = min(B, slots);
     // The hardware already refills a slot as soon as its workgroup retires, but only from its
@@ -1853,7 +1456,7 @@ static void launch_solve_ppt(const SolveArgs& a, int B, int lds, hipStream_t s) 
 
 // Points per thread held in registers by the objective: one for the LDS-mode kernels (C1-C3:
 // N <= 256; C3 +12% over re-reading x, d and the gradient from LDS per view).  Larger N, GV
-// mode and DAVA_NO_PPT take the re-reading variant: eight points per thread at C5 spill
+// mode and the kDbgNoPPT override take the re-reading variant: eight points per thread at C5 spill
 // (1 KB of scratch per lane) and ran 42% slower.
 // One-wave workgroups (one problem per wave) hold two points per lane (N <= 128).
 template <bool GV, bool XL, int NW>
@@ -1862,7 +1465,7 @@ constexpr int kRegisterPoints = GV ? 0 : (NW == 1 ? 2 : 1);
 template <int MODE, bool GV, int RES, bool XL, int NW>
 static void launch_solve_nw(const SolveArgs& a, int B, int lds, hipStream_t s) {
   constexpr int R = kRegisterPoints<GV, XL, NW>;
-  if (R > 0 && a.L.N <= R * kWave * NW && getenv("DAVA_NO_PPT") == nullptr)
+  if (R > 0 && a.L.N <= R * kWave * NW && !debug_flag(kDbgNoPPT))
     launch_solve_ppt<MODE, GV, RES, XL, R, NW>(a, B, lds, s);
   else
     launch_solve_ppt<MODE, GV, RES, XL, 0, NW>(a, B, lds, s);
@@ -1928,7 +1531,7 @@ static int solve_impl(const DavaScene* scene, const DavaSolverConfig* config, co
   if (uses_ws && (!workspace || workspace_bytes < need)) return DAVA_ERR_WORKSPACE;
   // the work queue needs its counter in the workspace's tail (dava_ba_solve_workspace_bytes
   // includes it); a workspace sized without it runs one workgroup per problem instead
-  const bool queue = workspace && workspace_bytes >= need + kQueueBytes && getenv("DAVA_NO_QUEUE") == nullptr;
+  const bool queue = workspace && workspace_bytes >= need + kQueueBytes && !debug_flag(kDbgNoQueue);
   SolveArgs a;
   a.L = Layout{scene->num_views, scene->num_points, scene->num_parameters, scene->distortion ? 1 : 0};
   a.B = scene->batch;

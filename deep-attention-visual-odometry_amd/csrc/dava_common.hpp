@@ -94,15 +94,12 @@ __device__ __forceinline__ void wave_sums(float (&v)[R]) {
 // so ONE barrier per reduction suffices (NW = waves in the workgroup): a wave cannot reach the next use of
 // the same buffer before every wave has passed the intervening reduction's
 // barrier, i.e. before every wave finished reading this one.
-#ifndef DAVA_TRANSPOSED_SUMS
-#define DAVA_TRANSPOSED_SUMS 1  // 0: one wave_sum per value (the round-1 form)
-#endif
 template <int R, int NW = kWaves>
 __device__ __forceinline__ void block_sum(float (&v)[R], float* scratch, int buf) {
   const int lane = threadIdx.x & (kWave - 1);
   const int wave = threadIdx.x / kWave;
   float* s = scratch + buf * (NW * 32);
-  if constexpr (DAVA_TRANSPOSED_SUMS && R >= 2) {
+  if constexpr (R >= 2) {
     float w[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) w[r] = v[r];

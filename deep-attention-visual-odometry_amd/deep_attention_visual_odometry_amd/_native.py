@@ -5,7 +5,14 @@ is deliberately NO fallback: if the library or a ROCm device is missing, every
 product entry point raises.  torch is imported first so the library binds to
 the HIP runtime torch already loaded (both carry SONAME libamdhip64.so.7),
 which lets it run on torch's streams and torch-allocated memory.
+
+Launch choices (LDS or global-vector mode, waves per workgroup, on-chip history entries, work queue,
+the generic loops below) are the library's own: neither it nor this module reads them from the
+environment, so a user's stray variable cannot change a launch.  Tests override them through
+:func:`debug_overrides`; A/B measurements set ``DAVA_DEBUG_OVERRIDES=1`` and the ``DAVA_<NAME>``
+variables, read ONCE when the library is loaded (``tools/ab_env.sh``).
 """
+import contextlib
 import ctypes
 import os
 import threading
@@ -13,7 +20,17 @@ import threading
 import torch  # noqa: F401  (must be loaded before the library, see above)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.environ.get("DAVA_LIB") or os.path.join(_HERE, "_lib", "libdava_ba.so")  # DAVA_LIB: A/B builds
+_DEBUG_ENV = os.environ.get("DAVA_DEBUG_OVERRIDES") == "1"  # the one gate: A/B and diagnostic runs only
+# DAVA_LIB (with the gate): another build of the library, for A/B runs (tools/build_prev.sh)
+LIB_PATH = (_DEBUG_ENV and os.environ.get("DAVA_LIB")) or os.path.join(_HERE, "_lib", "libdava_ba.so")
+
+# Overridable launch choices of the library (csrc/dava_debug.hpp), and of this package's Python side
+LIBRARY_KNOBS = ("FORCE_GV", "GV_NO_XL", "SOLVE_WAVES", "WG_PER_CU", "LDS_HISTORY", "STAGGER", "STAGGER_LEVELS",
+                 "NO_PPT", "NO_QUEUE", "ADJ_GV_WAVES", "ADJ_FORCE_GV", "ADJ_LDS_ENTRIES", "ADJ_GD_HBM")
+# GENERIC_BACKWARD: differentiate a fused objective's solve with the generic loop, not the adjoint;
+# GENERIC_TRAINING: training mode's drop path with the generic loop and torch's own RNG
+PYTHON_KNOBS = ("GENERIC_BACKWARD", "GENERIC_TRAINING")
+_py_knobs = {k: -1 for k in PYTHON_KNOBS}
 
 DAVA_OK = 0
 DAVA_HESSIAN_DENSE = 0
@@ -85,6 +102,8 @@ SIGNATURES = {
     "dava_ba_solve_backward": (ctypes.c_int, [ctypes.POINTER(DavaScene), ctypes.POINTER(DavaSolverConfig), _vp,
                                               ctypes.c_size_t, _vp, _vp, _vp, _vp, _vp, ctypes.c_size_t, _vp]),
     "dava_ba_solve_backward_lds_entries": (ctypes.c_int, [ctypes.POINTER(DavaScene), ctypes.POINTER(DavaSolverConfig)]),
+    "dava_debug_set_override": (ctypes.c_int, [ctypes.c_char_p, _c_i64]),
+    "dava_debug_clear_overrides": (None, []),
     "dava_abi_version": (ctypes.c_int, []),
     "dava_status_string": (ctypes.c_char_p, [ctypes.c_int]),
     "dava_device_arch": (ctypes.c_char_p, []),
@@ -129,7 +148,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
                 "(or __graft_entry__.build()); there is no CPU fallback")
         lib = ctypes.CDLL(path)
         for name, (res, args) in SIGNATURES.items():
-            if os.environ.get("DAVA_LIB") and not hasattr(lib, name):
+            if path != _DEFAULT_LIB and not hasattr(lib, name):
                 continue  # an older A/B build (tools/build_prev.sh) may predate some entry points
             fn = getattr(lib, name)
             fn.restype = res
@@ -137,7 +156,57 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         if lib.dava_abi_version() != ABI_VERSION:
             raise NativeLibraryError("libdava_ba.so ABI version mismatch")
         _lib = lib
+        if _DEBUG_ENV:  # A/B runs: the DAVA_<NAME> variables, read once, here
+            for k in LIBRARY_KNOBS + PYTHON_KNOBS:
+                v = os.environ.get("DAVA_" + k)
+                if v is None:
+                    continue
+                v = int(v) if v.lstrip("-").isdigit() else 1
+                if k in PYTHON_KNOBS:
+                    _py_knobs[k] = v
+                elif hasattr(lib, "dava_debug_set_override"):
+                    lib.dava_debug_set_override(k.encode(), v)
         return lib
+
+
+_DEFAULT_LIB = os.path.join(_HERE, "_lib", "libdava_ba.so")
+
+
+def set_debug_override(name: str, value: int) -> None:
+    """Override one launch choice (LIBRARY_KNOBS, PYTHON_KNOBS); value < 0 restores the default."""
+    if name in PYTHON_KNOBS:
+        _py_knobs[name] = int(value) if value >= 0 else -1
+        return
+    if name not in LIBRARY_KNOBS:
+        raise ValueError(f"unknown override {name!r}")
+    lib = load_library()
+    if hasattr(lib, "dava_debug_set_override"):
+        check(lib.dava_debug_set_override(name.encode(), int(value)), "dava_debug_set_override")
+
+
+def clear_debug_overrides() -> None:
+    for k in PYTHON_KNOBS:
+        _py_knobs[k] = -1
+    lib = load_library()
+    if hasattr(lib, "dava_debug_clear_overrides"):
+        lib.dava_debug_clear_overrides()
+
+
+def python_knob(name: str) -> bool:
+    """Is the Python-side override `name` (PYTHON_KNOBS) switched on?"""
+    return _py_knobs[name] > 0
+
+
+@contextlib.contextmanager
+def debug_overrides(**knobs):
+    """with debug_overrides(FORCE_GV=1, SOLVE_WAVES=2): ... -- tests only; cleared on exit."""
+    try:
+        for k, v in knobs.items():
+            set_debug_override(k, int(v))
+        yield
+    finally:
+        for k in knobs:
+            set_debug_override(k, -1)
 
 
 def check(status: int, what: str) -> None:

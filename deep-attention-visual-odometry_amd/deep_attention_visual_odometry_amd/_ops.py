@@ -20,7 +20,7 @@ from torch import Tensor
 from . import _native as N
 
 _CUDA = "cuda"
-_POISON = bool(__import__("os").environ.get("DAVA_POISON_SCRATCH"))  # fill tapes / workspaces with NaN first
+_POISON = N._DEBUG_ENV and bool(__import__("os").environ.get("DAVA_POISON_SCRATCH"))  # NaN-filled tapes (diagnostics)
 
 
 def _dt(t: Tensor) -> str:

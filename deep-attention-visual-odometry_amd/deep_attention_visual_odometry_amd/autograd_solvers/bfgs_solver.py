@@ -30,7 +30,6 @@ keeps x before its last step); when the reference's scatter would have moved row
 
 Not supported (raises rather than silently falling back): CPU tensors.
 """
-import os
 from typing import Callable, Optional
 
 import torch
@@ -108,7 +107,7 @@ class BFGSSolver(Module):
         # return_second_last (:196-212) unless the reference's scatter would move rows between problems
         drop_p = self.drop_path_p if self.training else 0.0
         second_last = self.training and self.return_second_last
-        generic_training = drop_p > 0.0 and bool(os.environ.get("DAVA_GENERIC_TRAINING"))  # torch-RNG generic loop
+        generic_training = drop_p > 0.0 and _native.python_knob("GENERIC_TRAINING")  # torch-RNG generic loop
         if isinstance(error_function, ReprojectionError) and not generic_training:
             seed = int(torch.randint(0, 2 ** 62, (1,)).item()) if drop_p > 0.0 else 0  # from torch's default generator
             out = None
@@ -122,36 +121,55 @@ class BFGSSolver(Module):
                 return out
             self.last_status = None  # the generic loop below has no status words
         if isinstance(error_function, ReprojectionError):
-            self._check_generic_fits(parameters, num_iterations)
+            self._check_generic_fits(parameters, num_iterations, second_last)
         return self._generic(parameters, error_function, error_threshold, num_iterations)
 
-    def _check_generic_fits(self, parameters, num_iterations) -> None:
-        """A fused objective that the fused kernels cannot take (differentiating a GV-mode solve,
-        P > 1024; dense mode or more than 1025 iterations with a graph; training mode's
-        return_second_last) runs the generic loop, which holds the reference's dense (B, P, P)
-        inverse Hessian -- and, with a graph, about three P x P tensors per problem per iteration.
-        Where that cannot fit the device, refuse up front instead of running out of memory midway."""
+    # dense (B, P, P) tensors the generic loop holds at once in its first iterations: the inverse
+    # Hessian, its masked gather / scatter copies and the update's temporaries (more with a graph)
+    _GENERIC_FIRST_MATRICES = 8
+
+    def _check_generic_fits(self, parameters, num_iterations, second_last=False) -> None:
+        """A fused objective the fused kernels cannot take runs the generic loop, which holds the
+        reference's dense (B, P, P) inverse Hessian -- and, with a graph, about three P x P tensors per
+        problem per ITERATION RUN (problems usually stop long before the cap: 36-107 iterations at
+        C2/C3 under the reference's defaults).  Refused up front only when even the first iterations
+        cannot fit the device; a run that would fit only if it stopped early gets a warning, and the
+        allocator reports an actual out-of-memory."""
+        import warnings
+
         lead = parameters.shape[:-1]
         b = max(int(torch.tensor(lead).prod().item()) if len(lead) else 1, 1)
         p = parameters.size(-1)
         per_matrix = b * p * p * parameters.element_size()
-        need = per_matrix * (3 * num_iterations + 2 if parameters.requires_grad else 8)
+        if parameters.requires_grad:
+            what = ("differentiating through the solve (dense mode or the GENERIC_BACKWARD override)"
+                    if self.hessian_mode == "dense" or _native.python_knob("GENERIC_BACKWARD")
+                    else "differentiating through the solve (no fused adjoint for this shape)")
+        elif second_last:
+            what = "training mode's return_second_last, whose scatter moves rows between problems"
+        else:
+            what = "the generic loop (GENERIC_TRAINING override)"
+        first = per_matrix * self._GENERIC_FIRST_MATRICES
         free = _free_device_bytes(parameters.device)
-        if need > free:
-            what = ("differentiating through the solve" if parameters.requires_grad
-                    else "training mode with return_second_last")
+        if first > free:
             raise RuntimeError(
-                f"{what} at B={b}, P={p}, {num_iterations} iterations has no fused kernel here (the adjoint covers "
-                f"compact mode with P <= 14336 and at most {self.MAX_COMPACT_ENTRIES + 1} iterations); the generic "
-                f"loop would hold the dense (B, P, P) inverse Hessian ~{need / 2 ** 30:.0f} GiB against "
-                f"{free / 2 ** 30:.0f} GiB free. Reduce the batch or the iteration count.")
+                f"{what} at B={b}, P={p} has no fused kernel here (the adjoint covers compact mode with "
+                f"P <= 14336 and at most {self.MAX_COMPACT_ENTRIES + 1} iterations); the generic loop's dense "
+                f"(B, P, P) inverse Hessian and its first temporaries alone need ~{first / 2 ** 30:.0f} GiB "
+                f"against {free / 2 ** 30:.0f} GiB free. Reduce the batch.")
+        cap = per_matrix * (3 * num_iterations + 2 if parameters.requires_grad else self._GENERIC_FIRST_MATRICES)
+        if cap > free:
+            warnings.warn(f"{what}: the generic loop needs ~{per_matrix * 3 / 2 ** 30:.1f} GiB more per iteration run "
+                          f"with a graph ({free / 2 ** 30:.0f} GiB free); it fits only if the problems stop "
+                          f"within ~{int((free / per_matrix - 2) / 3)} of the {num_iterations} iterations",
+                          RuntimeWarning, stacklevel=3)
 
     def _adjoint_available(self, parameters, fn: ReprojectionError, num_iterations) -> bool:
         """Differentiating through a fused objective's solve runs the recording solve + adjoint
         kernel (compact history; P <= 14336: C1-C3 with the O(P) vectors in LDS, C5 with them in
         HBM) unless dense mode was asked for or
-        DAVA_GENERIC_BACKWARD is set (then: the generic loop, graph kept by torch)."""
-        if self.hessian_mode == "dense" or os.environ.get("DAVA_GENERIC_BACKWARD"):
+        the GENERIC_BACKWARD override is on (then: the generic loop, graph kept by torch; _native.debug_overrides)."""
+        if self.hessian_mode == "dense" or _native.python_knob("GENERIC_BACKWARD"):
             return False
         if parameters.dtype != torch.float32 or num_iterations < 1 or num_iterations > self.MAX_COMPACT_ENTRIES + 1:
             return False

@@ -110,11 +110,13 @@ def second_last_moves_rows(status: torch.Tensor) -> bool:
 
 def solve_tape_supported(batch: int, num_views: int, num_points: int, distortion: bool, iterations: int,
                          residual: int = N.DAVA_RESIDUAL_SQUARED_REPROJECTION) -> bool:
-    """Host-only: does this shape have the fused adjoint (``dava_ba_solve_tape_bytes`` > 0)?"""
+    """Host-only: does this shape have the fused adjoint -- a recording forward
+    (``dava_ba_solve_tape_bytes`` > 0) AND a backward that can launch on it
+    (``dava_ba_solve_backward_workspace_bytes`` > 0)?"""
     lib = N.load_library()
     sc = scene_struct(None, None, num_views, num_points, distortion, max(int(batch), 1), residual)
     cfg = solver_config(1e-4, 0.9, 1e-4, iterations, 1e-8, 1000, True, N.DAVA_HESSIAN_COMPACT)
-    return int(lib.dava_ba_solve_tape_bytes(sc, cfg)) > 0
+    return int(lib.dava_ba_solve_tape_bytes(sc, cfg)) > 0 and int(lib.dava_ba_solve_backward_workspace_bytes(sc, cfg)) > 0
 
 
 class _FusedSolve(torch.autograd.Function):

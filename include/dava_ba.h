@@ -150,8 +150,10 @@ int dava_ba_solve(const DavaScene* scene, const DavaSolverConfig* config, const 
  * line search's step size a constant) without a dense (B, P, P) inverse Hessian per iteration.
  * A recording solve keeps a tape in HBM (x_k, g_k, the compact history rows, step sizes; see
  * csrc/dava_tape.hpp); the adjoint replays it backwards, one workgroup per problem.
- * COMPACT mode, P <= 1024 with the O(P) state in LDS (C1-C3 shapes); otherwise the size
- * queries return 0 and the calls DAVA_ERR_UNSUPPORTED. */
+ * COMPACT mode only, iterations <= 1025 and P <= 14336: shapes whose O(P) state fits the LDS
+ * (C1-C3) keep it there, larger ones (the forward's global-vector mode, e.g. C5 with P = 12381)
+ * keep it in the adjoint's workspace.  Otherwise the size queries return 0 and the calls
+ * DAVA_ERR_UNSUPPORTED. */
 
 /* Bytes of the tape (including the work-queue counter's 256 bytes), or 0 if unsupported. */
 size_t dava_ba_solve_tape_bytes(const DavaScene* scene, const DavaSolverConfig* config);
@@ -325,6 +327,16 @@ int dava_l1_camera_vjp_f64(int64_t batch, int32_t estimates, int32_t views, int3
                            double minimum_z_distance, double inverse_pixel_ratio, double max_gradient,
                            double error_scale, const double* error_cotangent, const double* gradient_cotangent,
                            int32_t detach_points, double* input_cotangent_out, void* stream);
+
+/* ---- test and A/B hooks ----
+ * The library makes its launch choices itself (LDS or global-vector mode, waves per workgroup,
+ * on-chip history entries, work queue, ...) and reads NOTHING from the environment.  Tests and A/B
+ * measurements override a choice by name (FORCE_GV, GV_NO_XL, SOLVE_WAVES, WG_PER_CU, LDS_HISTORY,
+ * STAGGER, STAGGER_LEVELS, NO_PPT, NO_QUEUE, ADJ_GV_WAVES, ADJ_FORCE_GV, ADJ_LDS_ENTRIES, ADJ_GD_HBM;
+ * csrc/dava_debug.hpp); value < 0 restores the library's choice.  Process-wide, not thread-safe,
+ * host-only.  DAVA_ERR_INVALID_ARGUMENT for an unknown name.                                     */
+int dava_debug_set_override(const char* name, int64_t value);
+void dava_debug_clear_overrides(void);
 
 /* ---- misc ---- */
 const char* dava_status_string(int status);

@@ -31,3 +31,14 @@ def device():
     if not torch.cuda.is_available():
         pytest.skip("no ROCm device")
     return torch.device("cuda", 0)
+
+
+@pytest.fixture()
+def overrides():
+    """overrides(name, value): one of the library's launch choices (or the Python side's generic-loop
+    switches) for this test, through _native.set_debug_override; every override is cleared afterwards.
+    The library never reads them from the environment."""
+    from deep_attention_visual_odometry_amd import _native
+
+    yield _native.set_debug_override
+    _native.clear_debug_overrides()

@@ -56,6 +56,11 @@ Fixtures written:
                           autograd), the BA objective with the distorted model (C1/C2/C3
                           shapes, fp32/fp64) and BFGSSolver().eval() on it after K = 5/20/100
                           at the headline shape (C3 + Brown-Conrady, fp32).
+* ``distortion_masked.npz`` -- the same model with 10 % of the (view, point) pairs masked:
+                          objective + gradient (C1/C2/C3, fp32/fp64), BFGSSolver().eval() after
+                          K = 5/20/100 at the headline shape, and BFGSSolver().eval() with the
+                          reference's DEFAULT stopping rules there and on distortion.npz's
+                          unmasked headline batch (converged parameters).
 * ``bfgs_traj.npz``   -- ``BFGSSolver(...).eval()`` results after K in
                           {5, 20, 100} iterations (error_threshold = -1,
                           minimum_step = -1) for C1 (2x64), C2 (2x128) and
@@ -685,11 +690,57 @@ def gen_distortion():
     np.savez_compressed(os.path.join(HERE, "distortion.npz"), **out)
 
 
+def gen_distortion_masked():
+    """The headline model under visibility masks, and run to the reference's own stopping rules.
+
+    The reference objective multiplies every pair's squared residual by its visibility
+    (calibration_network.py:58-67); 10 % of the (view, point) pairs are masked here.  Eager-mode
+    reference (the oracle's bitwise target): the objective and its gradient (C1/C2/C3 shapes,
+    fp32/fp64), BFGSSolver().eval() after K = 5/20/100 at the headline shape (C3 + Brown-Conrady,
+    fp32), and BFGSSolver().eval() with the reference's DEFAULT stopping rules (error 1e-4,
+    1000 iterations, minimum step 1e-8, bfgs_solver.py:53-55) on the masked batch and on the
+    unmasked headline batch of distortion.npz (converged parameters)."""
+    eager = reference_distorted_model(False)
+    out = {}
+    for name, (m, n) in SHAPES.items():
+        for dt_name, dt in (("f64", torch.float64), ("f32", torch.float32)):
+            s = make_scenes(1, m, n, distortion=True, seed=7511, drop=0.1)
+            obs, vis = torch.tensor(s.observations, dtype=dt), torch.tensor(s.visibility)
+            assert not vis.all()
+            x = torch.tensor(s.initial, dtype=dt, requires_grad=True)
+            e = ref_objective_bc(x, obs, vis, m, n, eager)
+            (g,) = torch.autograd.grad(e.sum(), x)
+            key = f"eval_{name}_{dt_name}"
+            out[key + "_err"], out[key + "_grad"] = e.detach().numpy(), g.numpy()
+            out[key + "_x"], out[key + "_obs"], out[key + "_vis"] = x.detach().numpy(), obs.numpy(), vis.numpy()
+    m, n = SHAPES["c3"]
+    s = make_scenes(8, m, n, distortion=True, seed=7512, drop=0.1)
+    x0, obs, vis = torch.tensor(s.initial), torch.tensor(s.observations), torch.tensor(s.visibility)
+    out["traj_c3m_x0"], out["traj_c3m_obs"], out["traj_c3m_vis"] = x0.numpy(), obs.numpy(), vis.numpy()
+
+    def fn(x, mask):
+        return ref_objective_bc(x, obs[mask], vis[mask], m, n, eager)
+
+    for k in (5, 20, 100):
+        out[f"traj_c3m_k{k}"] = BFGSSolver(iterations=k, error_threshold=-1.0, minimum_step=-1.0).eval()(x0, fn).numpy()
+    out["traj_c3m_default"] = BFGSSolver().eval()(x0, fn).numpy()
+    g = np.load(os.path.join(HERE, "distortion.npz"))
+    x0u, obsu, visu = (torch.tensor(g["traj_c3_x0"]), torch.tensor(g["traj_c3_obs"]), torch.tensor(g["traj_c3_vis"]))
+
+    def fnu(x, mask):
+        return ref_objective_bc(x, obsu[mask], visu[mask], m, n, eager)
+
+    out["traj_c3_default"] = BFGSSolver().eval()(x0u, fnu).numpy()
+    np.savez_compressed(os.path.join(HERE, "distortion_masked.npz"), **out)
+
+
 if __name__ == "__main__":
     torch.set_num_threads(8)
-    which = sys.argv[1:] or ["eval", "update", "ls", "traj", "ray", "grad", "train", "l1", "l1grad", "bc"]
+    which = sys.argv[1:] or ["eval", "update", "ls", "traj", "ray", "grad", "train", "l1", "l1grad", "bc", "bcmask"]
     if "bc" in which:
         gen_distortion()
+    if "bcmask" in which:
+        gen_distortion_masked()
     if "eval" in which:
         gen_ba_eval()
     if "update" in which:

@@ -216,7 +216,7 @@ def test_second_order_kernel_matches_double_backward(device, residual, distortio
 
 @pytest.mark.parametrize("path", ["fused", "generic"])
 @pytest.mark.parametrize("name", ["ba32", "ray32"])
-def test_gradient_through_a_fused_objective_solve_matches_reference(device, name, path, monkeypatch):
+def test_gradient_through_a_fused_objective_solve_matches_reference(device, name, path, overrides):
     """BFGSSolver with ReprojectionError / RayAngleError as the closure and x0, obs requiring
     grad: d loss/d x0 and d loss/d obs through K = 5 iterations vs the REAL reference's
     autograd (fp32 on both sides; the GPU's reduction order differs, hence 1e-3).  "fused": the
@@ -225,7 +225,7 @@ def test_gradient_through_a_fused_objective_solve_matches_reference(device, name
     from deep_attention_visual_odometry_amd import RayAngleError, ReprojectionError
 
     if path == "generic":
-        monkeypatch.setenv("DAVA_GENERIC_BACKWARD", "1")
+        overrides("GENERIC_BACKWARD", 1)
     g = np.load(os.path.join(GOLDEN, "solve_grad.npz"))
     x0 = torch.tensor(g[name + "_x0"], device=device, requires_grad=True)
     obs = torch.tensor(g[name + "_obs"], device=device, requires_grad=True)
@@ -311,12 +311,10 @@ def test_fused_adjoint_matches_oracle(device, m, n, distortion, ray, k, b):
         # reduction order moves second-order terms far more than for the squared objective: hold the
         # adjoint to 4x the generic loop's own distance from the oracle (op-by-op the reference's),
         # at least 2e-2 (one problem has measured 5e-3 on one box and 3e-5 on others)
-        import os as _os
-        _os.environ["DAVA_GENERIC_BACKWARD"] = "1"
-        try:
+        from deep_attention_visual_odometry_amd import _native
+
+        with _native.debug_overrides(GENERIC_BACKWARD=1):
             _, gx_g, go_g, _ = _fused_grads(device, x0, obs, vis, m, n, distortion, w, ray, **kw)
-        finally:
-            del _os.environ["DAVA_GENERIC_BACKWARD"]
         tol_x = torch.maximum(torch.full_like(rx, 2e-2), 4.0 * _rows_rel(gx_g, gx_ref))
         tol_o = torch.maximum(torch.full_like(ro, 2e-2), 4.0 * _rows_rel(go_g, go_ref))
     print("ADJOINT", m, n, distortion, ray, k, "x0", rx.max().item(), "obs", ro.max().item(),
@@ -372,7 +370,7 @@ def test_recording_tape_is_deterministic(device):
     assert torch.equal(tape, first)
 
 
-def test_adjoint_on_chip_history_is_bitwise_invisible(device, monkeypatch):
+def test_adjoint_on_chip_history_is_bitwise_invisible(device, overrides):
     """The adjoint's LDS-held history entries (dava_ba_solve_backward_lds_entries) change where rows
     are read from, not the arithmetic: 0, 3 and the default count give identical gradients."""
     from deep_attention_visual_odometry_amd import make_scenes, native_ops
@@ -390,15 +388,15 @@ def test_adjoint_on_chip_history_is_bitwise_invisible(device, monkeypatch):
     runs = []
     for cap in (None, "0", "3"):
         if cap is None:
-            monkeypatch.delenv("DAVA_ADJ_LDS_ENTRIES", raising=False)
+            overrides("ADJ_LDS_ENTRIES", -1)
         else:
-            monkeypatch.setenv("DAVA_ADJ_LDS_ENTRIES", cap)
+            overrides("ADJ_LDS_ENTRIES", int(cap))
         runs.append(torch.ops.dava.ba_solve_backward(w, tape, status, obs, vis, m, n, True, k, 0, True))
     for gx, gobs in runs[1:]:
         assert torch.equal(gx, runs[0][0]) and torch.equal(gobs, runs[0][1])
 
 
-def test_fused_and_generic_backward_agree_c3(device, monkeypatch):
+def test_fused_and_generic_backward_agree_c3(device, overrides):
     """C3 + Brown-Conrady, K = 30: the adjoint kernel and the generic loop (dense H per iteration in
     torch's graph, HIP VJP kernels) give the same gradients."""
     from deep_attention_visual_odometry_amd import make_scenes
@@ -408,7 +406,7 @@ def test_fused_and_generic_backward_agree_c3(device, monkeypatch):
     w = torch.randn(x0.shape, generator=torch.Generator().manual_seed(2))
     kw = dict(iterations=30, error_threshold=-1.0, minimum_step=-1.0)
     out, gx, go, _ = _fused_grads(device, x0, obs, vis, 4, 256, True, w, **kw)
-    monkeypatch.setenv("DAVA_GENERIC_BACKWARD", "1")
+    overrides("GENERIC_BACKWARD", 1)
     out_g, gx_g, go_g, _ = _fused_grads(device, x0, obs, vis, 4, 256, True, w, hessian_mode="compact", **kw)
     assert _rows_rel(out, out_g).max() <= 1e-5
     assert _rows_rel(gx, gx_g).max() <= 2e-3
@@ -466,7 +464,7 @@ def test_fused_adjoint_through_a_training_mode_solve(device):
 # vectors live in its workspace and its passes run workgroup-wide (csrc/bfgs_adjoint.hip, GT > 0) ----
 
 @pytest.mark.parametrize("ray", [False, True])
-def test_gv_adjoint_matches_lds_adjoint(device, ray, monkeypatch):
+def test_gv_adjoint_matches_lds_adjoint(device, ray, overrides):
     """One C3-shaped tape replayed by both adjoint kernels (DAVA_ADJ_FORCE_GV): the same math with
     the vectors in HBM and a different summation order -- gradients agree to fp32 reordering."""
     from deep_attention_visual_odometry_amd import make_scenes
@@ -481,7 +479,7 @@ def test_gv_adjoint_matches_lds_adjoint(device, ray, monkeypatch):
                                                      res)
     assert (status[:, 0] == k).all() and torch.isfinite(x).all()
     gx, gobs = torch.ops.dava.ba_solve_backward(w, tape, status, obs, vis, m, n, dist, k, res, True)
-    monkeypatch.setenv("DAVA_ADJ_FORCE_GV", "1")
+    overrides("ADJ_FORCE_GV", 1)
     gx_gv, gobs_gv = torch.ops.dava.ba_solve_backward(w, tape, status, obs, vis, m, n, dist, k, res, True)
     rx, ro = _rows_rel(gx_gv.cpu(), gx.cpu()), _rows_rel(gobs_gv.cpu(), gobs.cpu())
     print("GV vs LDS adjoint", "ray" if ray else "sq", rx.max().item(), ro.max().item())
@@ -492,14 +490,14 @@ def test_gv_adjoint_matches_lds_adjoint(device, ray, monkeypatch):
 
 
 @pytest.mark.parametrize("waves,gd_hbm", [("4", False), ("8", True)])
-def test_gv_adjoint_forms_agree(device, waves, gd_hbm, monkeypatch):
+def test_gv_adjoint_forms_agree(device, waves, gd_hbm, overrides):
     """The global-vector adjoint's variants -- four waves with 14 groups per thread, and eight waves
     with the HVP's dual gradient in the workspace instead of LDS -- against the default (eight waves,
     dual gradient in LDS) on one C3-shaped tape: the same math in another summation order (four vs
     eight waves) or bit for bit (where the dual gradient lives)."""
     from deep_attention_visual_odometry_amd import make_scenes
 
-    monkeypatch.setenv("DAVA_ADJ_FORCE_GV", "1")
+    overrides("ADJ_FORCE_GV", 1)
     m, n, k = 4, 256, 24
     s = make_scenes(8, m, n, distortion=True, seed=938, drop=0.0)
     x0, obs, vis = (torch.tensor(t).to(device) for t in (s.initial, s.observations, s.visibility))
@@ -508,9 +506,9 @@ def test_gv_adjoint_forms_agree(device, waves, gd_hbm, monkeypatch):
     x, status, tape = torch.ops.dava.ba_solve_record(x0, obs, vis, m, n, True, 1e-4, 0.9, -1.0, k, -1.0, 1000, True, 0)
     assert (status[:, 0] == k).all() and torch.isfinite(x).all()
     gx, gobs = torch.ops.dava.ba_solve_backward(w, tape, status, obs, vis, m, n, True, k, 0, True)
-    monkeypatch.setenv("DAVA_ADJ_GV_WAVES", waves)
+    overrides("ADJ_GV_WAVES", int(waves))
     if gd_hbm:
-        monkeypatch.setenv("DAVA_ADJ_GD_HBM", "1")
+        overrides("ADJ_GD_HBM", 1)
     gx2, gobs2 = torch.ops.dava.ba_solve_backward(w, tape, status, obs, vis, m, n, True, k, 0, True)
     if waves == "8":
         assert torch.equal(gx2, gx) and torch.equal(gobs2, gobs)
@@ -519,13 +517,13 @@ def test_gv_adjoint_forms_agree(device, waves, gd_hbm, monkeypatch):
         assert rx.max() <= 1e-4 and ro.max() <= 1e-4, (rx, ro)
 
 
-def test_gv_recording_is_bitwise_the_gv_solve(device, monkeypatch):
+def test_gv_recording_is_bitwise_the_gv_solve(device, overrides):
     """A global-vector-mode recording (DAVA_FORCE_GV at the C3 shape: the forward's vectors in the
     tape's own region, wide history pass writing the tape rows) returns exactly the GV solve's x and
     status."""
     from deep_attention_visual_odometry_amd import make_scenes, native_ops
 
-    monkeypatch.setenv("DAVA_FORCE_GV", "1")
+    overrides("FORCE_GV", 1)
     s = make_scenes(16, 4, 256, distortion=True, seed=937, drop=0.0)
     x0, obs, vis = (torch.tensor(t).to(device) for t in (s.initial, s.observations, s.visibility))
     kw = dict(iterations=30, error_threshold=-1.0, minimum_step=-1.0)
@@ -539,14 +537,14 @@ def test_gv_recording_is_bitwise_the_gv_solve(device, monkeypatch):
     (4, 400, False, False, 10, 2),  # P = 1221 > 1024: LDS-mode forward, GV adjoint
     (3, 1300, True, False, 6, 1),   # P = 3920: GV forward (wide pass, GT = 2), ragged points per thread
 ])
-def test_gv_adjoint_matches_oracle(device, m, n, distortion, force_gv, k, b, monkeypatch):
+def test_gv_adjoint_matches_oracle(device, m, n, distortion, force_gv, k, b, overrides):
     """d (w . x_K) / d x0 and / d obs through a solve whose adjoint runs in global-vector mode, vs
     autograd through the oracle's fp32 restatement of the reference's loop (create_graph)."""
     from deep_attention_visual_odometry_amd import make_scenes
 
     if force_gv:
-        monkeypatch.setenv("DAVA_FORCE_GV", "1")
-        monkeypatch.setenv("DAVA_ADJ_FORCE_GV", "1")
+        overrides("FORCE_GV", 1)
+        overrides("ADJ_FORCE_GV", 1)
     s = make_scenes(b, m, n, distortion=distortion, seed=950 + n + k, drop=0.0 if distortion else 0.1)
     x0, obs, vis = torch.tensor(s.initial), torch.tensor(s.observations), torch.tensor(s.visibility)
     w = torch.randn(x0.shape, generator=torch.Generator().manual_seed(k))

@@ -241,18 +241,15 @@ def test_reference_golden_distorted_trajectories(device, mode):
 
 
 def test_default_stopping_rules(device):
-    """Reference defaults (error 1e-4, 1000 iterations, min step 1e-8): the objective reached
-    matches the oracle's, and every problem stops by a rule, not the cap."""
+    """Reference defaults (error 1e-4, 1000 iterations, min step 1e-8) on C1 shapes: every problem
+    stops by a rule at the oracle's iteration for the oracle's reason, parameters per _converged_check."""
     x0, obs, vis = _scene(4, 2, 64, False, 321)
     out, status = _gpu_solve(device, x0, obs, vis, 2, 64, False)
     fn = objective.ReprojectionClosure(obs, vis, 2, 64)
     rec = solver.SolveRecord(None, None)
     ref = solver.bfgs_solve(x0, fn, record=rec)
-    e_gpu = objective.reprojection_error(out.double(), obs.double(), vis, 2, 64)
-    e_ref = objective.reprojection_error(ref.double(), obs.double(), vis, 2, 64)
-    assert (e_gpu <= 1e-4 + 1e-6).all() or (status[:, 1] != 0).all()
     assert (status[:, 1] != 0).all()
-    assert torch.allclose(e_gpu, e_ref, rtol=0.5, atol=1e-4)
+    _converged_check("defaults_C1_B4", out, status, ref, rec, x0, fn, obs, vis, 2, 64, distortion=False)
 
 
 def test_error_threshold_stops_immediately(device):
@@ -334,7 +331,7 @@ def test_c5_shape_global_vector_mode_matches_oracle(device):
 
 
 @pytest.mark.parametrize("xl", [True, False])
-def test_global_vector_packed_sweep_ragged_points_match_oracle(device, xl, monkeypatch):
+def test_global_vector_packed_sweep_ragged_points_match_oracle(device, xl, overrides):
     """GV mode's packed pair sweep (two of a thread's points per step) with a ragged point count
     (1300 points over 512 threads: some threads hold a pair plus a scalar tail, the rest one pair)
     and Brown-Conrady on, which C5 itself does not exercise; objective on LDS copies (XL) or on
@@ -343,7 +340,7 @@ def test_global_vector_packed_sweep_ragged_points_match_oracle(device, xl, monke
     kw = dict(iterations=10, error_threshold=-1.0, minimum_step=-1.0)
     ref = solver.bfgs_solve(x0, objective.ReprojectionClosure(obs, vis, 3, 1300, True), **kw)
     if not xl:
-        monkeypatch.setenv("DAVA_GV_NO_XL", "1")
+        overrides("GV_NO_XL", 1)
     for mode in ("compact", "dense"):
         out, status = _gpu_solve(device, x0, obs, vis, 3, 1300, True, hessian_mode=mode, **kw)
         assert _rel(out, ref).max() <= TOL, (mode, _rel(out, ref))
@@ -368,24 +365,24 @@ def test_c5_shape_objective_matches_oracle(device):
 
 @pytest.mark.parametrize("xl", [True, False])
 @pytest.mark.parametrize("mode", ["dense", "compact"])
-def test_global_vector_mode_equals_lds_mode(device, mode, xl, monkeypatch):
+def test_global_vector_mode_equals_lds_mode(device, mode, xl, overrides):
     """The same C3-shaped solve with the O(P) state forced into HBM (DAVA_FORCE_GV) agrees with
     the LDS-resident kernel (same device code, different memory), with the objective on LDS
     copies of x and d (the default where they fit) or on the workspace vectors (DAVA_GV_NO_XL)."""
     x0, obs, vis = _scene(8, 4, 256, True, 557)
     kw = dict(iterations=30, error_threshold=-1.0, minimum_step=-1.0, hessian_mode=mode)
     lds, _ = _gpu_solve(device, x0, obs, vis, 4, 256, True, **kw)
-    monkeypatch.setenv("DAVA_FORCE_GV", "1")
+    overrides("FORCE_GV", 1)
     if not xl:
-        monkeypatch.setenv("DAVA_GV_NO_XL", "1")
+        overrides("GV_NO_XL", 1)
     gv, _ = _gpu_solve(device, x0, obs, vis, 4, 256, True, **kw)
-    monkeypatch.delenv("DAVA_FORCE_GV")
-    monkeypatch.delenv("DAVA_GV_NO_XL", raising=False)
+    overrides("FORCE_GV", -1)
+    overrides("GV_NO_XL", -1)
     assert _rel(gv, lds).max() <= TOL
 
 
 @pytest.mark.parametrize("stopping", ["fixed", "reference"])
-def test_work_queue_launch_is_bitwise_invisible(device, stopping, monkeypatch):
+def test_work_queue_launch_is_bitwise_invisible(device, stopping, overrides):
     """More problems than resident workgroups: with the work queue (a slot takes the next
     problem when it finishes one) every problem's result and status are bitwise those of one
     workgroup per problem (DAVA_NO_QUEUE).  2048 C1-shaped problems exceed the chip's slots,
@@ -393,9 +390,9 @@ def test_work_queue_launch_is_bitwise_invisible(device, stopping, monkeypatch):
     x0, obs, vis = _scene(2048, 2, 64, False, 559)
     kw = dict(iterations=30, error_threshold=-1.0, minimum_step=-1.0) if stopping == "fixed" else dict(iterations=200)
     out, st = _gpu_solve(device, x0, obs, vis, 2, 64, False, hessian_mode="compact", **kw)
-    monkeypatch.setenv("DAVA_NO_QUEUE", "1")
+    overrides("NO_QUEUE", 1)
     ref, st_ref = _gpu_solve(device, x0, obs, vis, 2, 64, False, hessian_mode="compact", **kw)
-    monkeypatch.delenv("DAVA_NO_QUEUE")
+    overrides("NO_QUEUE", -1)
     assert torch.equal(out, ref)
     assert torch.equal(st, st_ref)
     if stopping == "reference":
@@ -403,24 +400,24 @@ def test_work_queue_launch_is_bitwise_invisible(device, stopping, monkeypatch):
         assert st[:, 0].unique().numel() > 1
 
 
-def test_staggered_start_is_bitwise_invisible(device, monkeypatch):
+def test_staggered_start_is_bitwise_invisible(device, overrides):
     """A launch whose problems are all resident at once starts its odd workgroups late (phases
     spread over the chip); timing only -- every result and status word is bitwise the same."""
     x0, obs, vis = _scene(256, 2, 128, False, 561)
     kw = dict(iterations=40, error_threshold=-1.0, minimum_step=-1.0, hessian_mode="compact")
     out, st = _gpu_solve(device, x0, obs, vis, 2, 128, False, **kw)
-    monkeypatch.setenv("DAVA_STAGGER", "0")
+    overrides("STAGGER", 0)
     ref, st_ref = _gpu_solve(device, x0, obs, vis, 2, 128, False, **kw)
-    monkeypatch.setenv("DAVA_STAGGER", "200000")
+    overrides("STAGGER", 200000)
     late, st_late = _gpu_solve(device, x0, obs, vis, 2, 128, False, **kw)
-    monkeypatch.delenv("DAVA_STAGGER")
+    overrides("STAGGER", -1)
     assert torch.equal(out, ref) and torch.equal(st, st_ref)
     assert torch.equal(late, ref) and torch.equal(st_late, st_ref)
 
 
 @pytest.mark.parametrize("waves", ["1", "2", "4"])
 @pytest.mark.parametrize("m,n,distortion,k", [(2, 64, False, 20), (2, 128, False, 20), (4, 256, True, 20)])
-def test_workgroup_waves_match_oracle(device, m, n, distortion, k, waves, monkeypatch):
+def test_workgroup_waves_match_oracle(device, m, n, distortion, k, waves, overrides):
     """One problem per 1-, 2- or 4-wave workgroup (DAVA_SOLVE_WAVES; the plan picks one per
     shape): the reduction trees differ, the parity bar against the oracle does not."""
     from deep_attention_visual_odometry_amd import native_ops
@@ -428,7 +425,7 @@ def test_workgroup_waves_match_oracle(device, m, n, distortion, k, waves, monkey
     x0, obs, vis = _scene(8, m, n, distortion, 600 + n + k)
     kw = dict(iterations=k, error_threshold=-1.0, minimum_step=-1.0)
     ref = solver.bfgs_solve(x0, objective.ReprojectionClosure(obs, vis, m, n, distortion), **kw)
-    monkeypatch.setenv("DAVA_SOLVE_WAVES", waves)
+    overrides("SOLVE_WAVES", int(waves))
     assert native_ops.solve_plan(8, m, n, distortion, 1, k)["workgroup_threads"] == 64 * int(waves)
     for mode in ("compact", "dense"):
         out, status = _gpu_solve(device, x0, obs, vis, m, n, distortion, hessian_mode=mode, **kw)
@@ -436,11 +433,11 @@ def test_workgroup_waves_match_oracle(device, m, n, distortion, k, waves, monkey
         _report(f"waves{waves}_{mode}_M{m}_N{n}_D{int(distortion)}_K{k}_B8", rel)
         assert rel.max() <= TOL, (mode, rel)
         assert (status[:, 0] == k).all()
-    monkeypatch.delenv("DAVA_SOLVE_WAVES")
+    overrides("SOLVE_WAVES", -1)
 
 
 @pytest.mark.parametrize("m,n,distortion", [(4, 256, True), (2, 128, False)])
-def test_lds_resident_history_is_bitwise_invisible(device, m, n, distortion, monkeypatch):
+def test_lds_resident_history_is_bitwise_invisible(device, m, n, distortion, overrides):
     """COMPACT mode keeps the oldest history entries on-chip (dava_ba_solve_plan); the products
     read the same values in the same order, so the result must not change by a single bit
     whether 0, the default or (past two workgroups per CU) 18 entries stay in LDS."""
@@ -451,12 +448,12 @@ def test_lds_resident_history_is_bitwise_invisible(device, m, n, distortion, mon
     assert native_ops.solve_plan(16, m, n, distortion, 1, 40)["lds_history_entries"] > 0
     ref, st_ref = _gpu_solve(device, x0, obs, vis, m, n, distortion, **kw)
     for entries in ("0", "18"):
-        monkeypatch.setenv("DAVA_LDS_HISTORY", entries)
+        overrides("LDS_HISTORY", int(entries))
         assert native_ops.solve_plan(16, m, n, distortion, 1, 40)["lds_history_entries"] == int(entries)
         out, st = _gpu_solve(device, x0, obs, vis, m, n, distortion, **kw)
         assert torch.equal(out, ref), entries
         assert torch.equal(st, st_ref), entries
-    monkeypatch.delenv("DAVA_LDS_HISTORY")
+    overrides("LDS_HISTORY", -1)
 
 
 # ---- ray-angle residual (CalibrationNetwork's error, calibration_network.py:58-67) ----
@@ -639,24 +636,23 @@ def test_fused_drop_path_is_the_eval_solve_stopped_early(device):
 
 def test_infeasible_generic_fallback_raises(device):
     """Differentiating a solve past the fused adjoint's reach (P = 15093 > 14336: more than 14 float4
-    groups per thread) falls to the generic loop, which would hold the dense (B, P, P) inverse Hessian
-    per iteration in the graph (hundreds of GiB): refused up front with a RuntimeError, never attempted."""
+    groups per thread) falls to the generic loop, whose dense (B, P, P) inverse Hessian and first
+    temporaries alone exceed the device here: refused up front with a RuntimeError, never attempted."""
     from deep_attention_visual_odometry_amd import BFGSSolver, ReprojectionError
 
-    m, n = 16, 5000
+    m, n, b = 16, 5000, 48  # 48 x 15093^2 x 4 B = 44 GB per dense matrix: the first iterations cannot fit
     p = 3 + 3 * n + 6 * (m - 1)
-    fn = ReprojectionError(torch.zeros(2, m, n, 2, device=device), torch.ones(2, m, n, device=device), m, n)
-    x0 = torch.zeros(2, p, device=device, requires_grad=True)
+    fn = ReprojectionError(torch.zeros(b, m, n, 2, device=device), torch.ones(b, m, n, device=device), m, n)
+    x0 = torch.zeros(b, p, device=device, requires_grad=True)
     with pytest.raises(RuntimeError, match="no fused kernel"):
         BFGSSolver(iterations=100, error_threshold=-1.0, minimum_step=-1.0).eval()(x0, fn)
 
 
 def test_reference_defaults_c2_objective_parity(device):
     """BFGSSolver() with the reference's DEFAULT kwargs (error 1e-4, 1000 iterations, min step 1e-8)
-    through the module on C2-shaped problems (runs to the stopping rules are judged by
-    the objective reached).  The module picks the compact history (the cap no longer forces the
-    dense matrix), every problem stops by a rule, and each reaches the oracle's objective (within
-    5%, or below the error threshold as the reference stops there)."""
+    through the module on C2-shaped problems.  The module picks the compact history (the cap no
+    longer forces the dense matrix), every problem stops by a rule -- at the oracle's iteration, for
+    the oracle's reason -- and its parameters are held to the fixed-K bar (_converged_check)."""
     from deep_attention_visual_odometry_amd import BFGSSolver, _native
 
     x0, obs, vis = _scene(16, 2, 128, False, 901)
@@ -666,14 +662,8 @@ def test_reference_defaults_c2_objective_parity(device):
     fn = objective.ReprojectionClosure(obs, vis, 2, 128)
     rec = solver.SolveRecord(None, None)
     ref = solver.bfgs_solve(x0, fn, record=rec)
-    e_gpu = objective.reprojection_error(out.double(), obs.double(), vis, 2, 128)
-    e_ref = objective.reprojection_error(ref.double(), obs.double(), vis, 2, 128)
-    _report("defaults_C2_B16", _rel(out, ref), None,
-            {"e_gpu_max": float(e_gpu.max()), "e_ref_max": float(e_ref.max()),
-             "steps_gpu_mean": float(status[:, 0].double().mean()),
-             "steps_ref_mean": float(rec.iterations.double().mean())})
     assert (status[:, 1] != 0).all()  # stopped by a rule, not the cap
-    assert (e_gpu <= 1.05 * torch.clamp(e_ref, min=1e-4)).all(), (e_gpu, e_ref)
+    _converged_check("defaults_C2_B16", out, status, ref, rec, x0, fn, obs, vis, 2, 128, distortion=False)
 
 
 # ---- training mode's return_second_last, fused (bfgs_solver.py:196-212) ----
@@ -804,3 +794,148 @@ def test_fused_second_last_gradient_matches_oracle(device):
         assert gx <= 2e-3 and go <= 2e-3, (i, gx, go)
         checked += 1
     assert checked >= 2
+
+
+# ---- the headline model under visibility masks, and run to the reference's stopping rules ----
+
+@pytest.mark.parametrize("mode", ["compact", "dense"])
+def test_reference_golden_masked_distorted_trajectories(device, mode):
+    """Against BFGSSolver().eval() of the REAL reference on the headline model with 10 % of the
+    (view, point) pairs masked (tests/golden/distortion_masked.npz, eager mode) after K = 5, 20, 100,
+    per block inside the reference's own 1-ulp envelopes.  Two of the eight problems overflow at a
+    trial point, where a masked pair contributes inf * 0 = NaN (calibration_network.py:58-67
+    multiplies by vis), and walk to NaN in the reference: the kernel must do the same to them."""
+    g = np.load(os.path.join(GOLDEN, "distortion_masked.npz"))
+    x0 = torch.tensor(g["traj_c3m_x0"])
+    obs, vis = torch.tensor(g["traj_c3m_obs"]), torch.tensor(g["traj_c3m_vis"])
+    assert not vis.all()
+    fn = objective.ReprojectionClosure(obs, vis, 4, 256, True)
+    for k in (5, 20, 100):
+        out, status = _gpu_solve(device, x0, obs, vis, 4, 256, True, iterations=k, error_threshold=-1.0,
+                                 minimum_step=-1.0, hessian_mode=mode)
+        ref = torch.tensor(g[f"traj_c3m_k{k}"])
+        finite = torch.isfinite(ref).all(dim=-1)
+        assert int(finite.sum()) == 6
+        assert torch.equal(torch.isfinite(out).all(dim=-1), finite)  # the same problems walk to NaN
+        kw = dict(iterations=k, error_threshold=-1.0, minimum_step=-1.0)
+        env, env_i, env_d = _envelopes(x0, fn, ref, distortion=True, **kw)
+        rel, rel_i, rel_d = _rel(out, ref), _rel(out[:, :3], ref[:, :3]), _rel(out[:, -5:], ref[:, -5:])
+        _report(f"golden_bc_masked_{mode}_c3_K{k}", rel[finite], env[finite],
+                {"distortion_max_rel": float(rel_d[finite].max()),
+                 "distortion_max_rel_over_envelope": float((rel_d / env_d)[finite].max())})
+        assert (rel <= env).all() and (rel <= TOL).all(), rel
+        assert (rel_i <= env_i).all(), rel_i
+        assert (rel_d <= env_d).all(), (rel_d, env_d)
+
+
+@pytest.mark.parametrize("k", [5, 20])
+def test_masked_distortion_matches_oracle(device, k):
+    """Brown-Conrady scenes with drop = 0.1 (masked pairs, the path no earlier BC test covered) at
+    the headline shape and a two-view shape, both inverse-Hessian modes, against the oracle."""
+    from deep_attention_visual_odometry_amd import make_scenes
+
+    for m, n, b in ((4, 256, 8), (2, 128, 16)):
+        s = make_scenes(b, m, n, distortion=True, seed=640 + k + n, drop=0.1)
+        x0, obs, vis = torch.tensor(s.initial), torch.tensor(s.observations), torch.tensor(s.visibility)
+        assert not vis.all()
+        kw = dict(iterations=k, error_threshold=-1.0, minimum_step=-1.0)
+        fn = objective.ReprojectionClosure(obs, vis, m, n, True)
+        ref = solver.bfgs_solve(x0, fn, **kw)
+        env, env_i, env_d = _envelopes(x0, fn, ref, distortion=True, **kw)
+        for mode in ("compact", "dense"):
+            out, status = _gpu_solve(device, x0, obs, vis, m, n, True, hessian_mode=mode, **kw)
+            rel, rel_d = _rel(out, ref), _rel(out[:, -5:], ref[:, -5:])
+            _report(f"bc_masked_{mode}_M{m}_N{n}_K{k}_B{b}", rel, env, {"distortion_max_rel": float(rel_d.max())})
+            assert (rel <= TOL).all() and (rel <= env).all(), (mode, rel)
+            assert (_rel(out[:, :3], ref[:, :3]) <= env_i).all()
+            assert (rel_d <= env_d).all(), (mode, rel_d, env_d)
+            assert (status[:, 0] == k).all()
+
+
+def _converged_check(tag, out, status, ref, rec, x0, fn, obs, vis, m, n, distortion=True):
+    """Converged parameters under the reference's default stopping rules (bfgs_solver.py:53-55).
+    Every finite problem must stop at the same iteration for the same reason as the reference, and
+    then its parameters are held to the fixed-K bar: per problem <= 1e-5 normwise and inside the
+    reference's own 1-ulp envelope for the whole vector, the intrinsics and the five distortion
+    coefficients; the objective reached to 1e-3 relative (E is a small residual at the stop, ~1e-4,
+    so a 1e-6 relative move of x can move it by far more than 1e-6 of itself)."""
+    finite = torch.isfinite(ref).all(dim=-1)
+    assert torch.equal(torch.isfinite(out).all(dim=-1), finite)
+    if distortion:
+        env, env_i, env_d = _envelopes(x0, fn, ref, distortion=True)
+    else:
+        (env, env_i), env_d = _envelopes(x0, fn, ref), torch.full((x0.shape[0],), float("inf"), dtype=torch.float64)
+    rel, rel_i, rel_d = _rel(out, ref), _rel(out[:, :3], ref[:, :3]), _rel(out[:, -5:], ref[:, -5:])
+    e_gpu = objective.reprojection_error(out.double(), obs.double(), vis, m, n, distortion)
+    e_ref = objective.reprojection_error(ref.double(), obs.double(), vis, m, n, distortion)
+    e_rel = ((e_gpu - e_ref).abs() / e_ref.abs())[finite]
+    _report(tag, rel[finite], env[finite],
+            {"intrinsics_max_rel": float(rel_i[finite].max()), "distortion_max_rel": float(rel_d[finite].max()),
+             "distortion_max_rel_over_envelope": float((rel_d / env_d)[finite].max()),
+             "objective_max_rel": float(e_rel.max()), "steps_mean": float(status[finite, 0].double().mean()),
+             "stop_reasons": sorted(set(status[finite, 1].tolist())),
+             "n_steps_differ": int((status[finite, 0] != rec.iterations[finite]).sum()),
+             "n_reason_differs": int((status[finite, 1] != rec.reason[finite]).sum())})
+    assert torch.equal(status[finite, 0], rec.iterations[finite]), (status[:, 0], rec.iterations)
+    assert torch.equal(status[finite, 1], rec.reason[finite]), (status[:, 1], rec.reason)
+    assert (rel <= env).all() and (rel <= TOL).all(), rel
+    assert (rel_i <= env_i).all(), rel_i
+    assert (rel_d <= env_d).all(), (rel_d, env_d)
+    assert (e_rel <= 1e-3).all(), e_rel
+
+
+def test_reference_golden_converged_distorted_parameters(device):
+    """BFGSSolver() with the reference's DEFAULT kwargs, through the module, on the headline model:
+    the converged parameters of the REAL reference (tests/golden/distortion_masked.npz: the unmasked
+    headline batch and the masked one), per block."""
+    from deep_attention_visual_odometry_amd import BFGSSolver
+
+    g = np.load(os.path.join(GOLDEN, "distortion_masked.npz"))
+    d = np.load(os.path.join(GOLDEN, "distortion.npz"))
+    for tag, x0, obs, vis, want in (
+            ("unmasked", d["traj_c3_x0"], d["traj_c3_obs"], d["traj_c3_vis"], g["traj_c3_default"]),
+            ("masked", g["traj_c3m_x0"], g["traj_c3m_obs"], g["traj_c3m_vis"], g["traj_c3m_default"])):
+        x0, obs, vis, want = (torch.tensor(a) for a in (x0, obs, vis, want))
+        fn = objective.ReprojectionClosure(obs, vis, 4, 256, True)
+        rec = solver.SolveRecord(None, None)
+        ref = solver.bfgs_solve(x0, fn, record=rec)
+        assert torch.equal(ref.isnan(), want.isnan()) and torch.equal(ref[~ref.isnan()], want[~want.isnan()])
+        s = BFGSSolver().eval()
+        assert s._resolve_mode(s.iterations, x0.shape[1], x0.shape[0], device) == 1  # compact
+        out, status = _gpu_solve(device, x0, obs, vis, 4, 256, True)
+        _converged_check(f"golden_bc_{tag}_defaults_c3", out, status, want, rec, x0, fn, obs, vis, 4, 256)
+
+
+def test_headline_converged_parameters_match_oracle(device):
+    """The bench's own headline problems (C3 + Brown-Conrady, first 16 of bench.py's batch) solved with
+    BFGSSolver() defaults through the module -- the north_star's "converged camera parameters within
+    1e-5 rel of reference" -- against the oracle run to the same stopping rules."""
+    h = _headline_reference()
+    fn = objective.ReprojectionClosure(h["obs"], h["vis"], 4, 256, True)
+    rec = solver.SolveRecord(None, None)
+    ref = solver.bfgs_solve(h["x0"], fn, record=rec)
+    out, status = _gpu_solve(device, h["x0"], h["obs"], h["vis"], 4, 256, True)
+    assert (status[:, 1] != 0).all()  # every problem stopped by a rule, not the cap
+    _converged_check("headline_defaults_C3_BC_B16", out, status, ref, rec, h["x0"], fn, h["obs"], h["vis"], 4, 256)
+
+
+def test_dense_mode_gradient_through_the_solve_runs_at_moderate_batch(device):
+    """hessian_mode='dense' with a graph runs the generic loop (the reference's own data structure):
+    C3 pinhole, B = 64, the reference's DEFAULT cap of 1000 iterations.  Its graph grows with the
+    iterations actually run (~107 here), not with the cap, so it must run (the earlier
+    cap-based estimate refused it) and give finite gradients, and its solve matches the fused one."""
+    import warnings
+
+    from deep_attention_visual_odometry_amd import BFGSSolver, ReprojectionError
+
+    x0, obs, vis = _scene(64, 4, 256, False, 905)
+    fn = ReprojectionError(obs.to(device), vis.to(device), 4, 256)
+    xd = x0.to(device).requires_grad_(True)
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore", RuntimeWarning)  # "fits only if the problems stop early"
+        out = BFGSSolver(hessian_mode="dense").eval()(xd, fn)
+    (g,) = torch.autograd.grad(out.square().sum(), xd)
+    assert torch.isfinite(out).all() and torch.isfinite(g).all()
+    fused = BFGSSolver().eval()(x0.to(device), fn)
+    rel = _rel(out.detach().cpu(), fused.cpu())
+    assert (rel <= 1e-4).float().mean() >= 0.9, rel

@@ -83,12 +83,12 @@ def test_workspace_size_dense(lib):
     assert native_ops.solve_workspace_bytes(8192, 4, 256, True) == 8192 * p * ((p + 31) // 32 * 32) * 4 + 256
 
 
-def test_solve_plan(lib, monkeypatch):
+def test_solve_plan(lib, overrides):
     """Host-only plan query: C3 keeps its oldest history entries in LDS within two workgroups
     per CU; C5 (P = 12381) runs the O(P) state from HBM in 512-thread workgroups."""
     from deep_attention_visual_odometry_amd import native_ops
 
-    monkeypatch.delenv("DAVA_LDS_HISTORY", raising=False)
+    overrides("LDS_HISTORY", -1)
     c3 = native_ops.solve_plan(8192, 4, 256, True, 1, 100)
     assert c3["global_vectors"] == 0 and c3["workgroup_threads"] == 256
     assert c3["lds_history_entries"] > 0 and c3["lds_bytes"] <= 80 * 1024
@@ -96,13 +96,13 @@ def test_solve_plan(lib, monkeypatch):
     c5 = native_ops.solve_plan(256, 16, 4096, False, 1, 100)
     assert c5["global_vectors"] == 1 and c5["workgroup_threads"] == 512 and c5["lds_history_entries"] == 0
     # two waves while a history row is at most 128 float4 column groups: C1 (P = 201), C2 (P = 393)
-    monkeypatch.delenv("DAVA_SOLVE_WAVES", raising=False)
+    overrides("SOLVE_WAVES", -1)
     assert native_ops.solve_plan(1024, 2, 64, False, 1, 100)["workgroup_threads"] == 128
     assert native_ops.solve_plan(1024, 2, 128, False, 1, 100)["workgroup_threads"] == 128
     assert native_ops.solve_plan(1024, 2, 128, False, 0, 100)["workgroup_threads"] == 256  # dense keeps 4
-    monkeypatch.setenv("DAVA_SOLVE_WAVES", "4")
+    overrides("SOLVE_WAVES", 4)
     assert native_ops.solve_plan(1024, 2, 64, False, 1, 100)["workgroup_threads"] == 256
-    monkeypatch.setenv("DAVA_LDS_HISTORY", "1000")  # clamped to one workgroup's LDS
+    overrides("LDS_HISTORY", 1000)  # clamped to one workgroup's LDS
     big = native_ops.solve_plan(8192, 4, 256, True, 1, 100)
     assert big["lds_bytes"] <= 160 * 1024 and big["lds_history_entries"] > c3["lds_history_entries"]
 
@@ -238,3 +238,82 @@ def test_operator_shape_checks_run_before_any_launch():
     with _pytest.raises(TypeError):
         _ops._check_scene_tensors(x, torch.zeros(2, 2, 16, 2, dtype=torch.float64),
                                   torch.zeros(2, 2, 16, dtype=torch.uint8), 2, 16, False)
+
+
+def test_launch_choices_ignore_the_environment():
+    """The library reads no environment and the binding reads the DAVA_<NAME> overrides only behind
+    DAVA_DEBUG_OVERRIDES=1: a user's stray DAVA_FORCE_GV / DAVA_SOLVE_WAVES / DAVA_LIB changes nothing."""
+    import json
+    import subprocess
+    import sys
+
+    from conftest import SRC
+
+    code = ("import sys, json; sys.path.insert(0, %r)\n"
+            "from deep_attention_visual_odometry_amd import native_ops, _native\n"
+            "print(json.dumps([native_ops.solve_plan(8192, 4, 256, True, 1, 100),"
+            " native_ops.solve_plan(1024, 2, 128, False, 1, 100), _native.LIB_PATH]))") % SRC
+    env = dict(os.environ, DAVA_FORCE_GV="1", DAVA_SOLVE_WAVES="4", DAVA_LIB="/nonexistent/libdava_ba.so",
+               DAVA_GENERIC_BACKWARD="1")
+    env.pop("DAVA_DEBUG_OVERRIDES", None)
+    c3, c2, path = json.loads(subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True,
+                                             check=True, timeout=120).stdout.strip().splitlines()[-1])
+    assert c3["global_vectors"] == 0 and c2["workgroup_threads"] == 128 and path.endswith("_lib/libdava_ba.so")
+    env.update(DAVA_DEBUG_OVERRIDES="1")
+    env.pop("DAVA_LIB")
+    c3, c2, _ = json.loads(subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True,
+                                          check=True, timeout=120).stdout.strip().splitlines()[-1])
+    assert c3["global_vectors"] == 1 and c2["global_vectors"] == 1  # the A/B gate: read once, at load
+
+
+def test_debug_overrides_are_scoped(lib):
+    from deep_attention_visual_odometry_amd import _native, native_ops
+
+    base = native_ops.solve_plan(8192, 4, 256, True, 1, 100)
+    with _native.debug_overrides(FORCE_GV=1, GENERIC_BACKWARD=1):
+        assert native_ops.solve_plan(8192, 4, 256, True, 1, 100)["global_vectors"] == 1
+        assert _native.python_knob("GENERIC_BACKWARD")
+    assert native_ops.solve_plan(8192, 4, 256, True, 1, 100) == base
+    assert not _native.python_knob("GENERIC_BACKWARD")
+    with pytest.raises(ValueError):
+        _native.set_debug_override("NOT_A_KNOB", 1)
+    assert lib.dava_debug_set_override(b"NOT_A_KNOB", 1) == 1
+
+
+@pytest.mark.parametrize("m", [200, 260, 300, 336])
+def test_adjoint_support_matches_its_launch_image(lib, m):
+    """Many views (the eight-wave global-vector image grows with the per-wave view partials): the size
+    queries accept a shape only if the launch that will run fits the LDS -- eight waves where they fit,
+    else four -- so a recorded forward never meets a backward that cannot launch."""
+    from deep_attention_visual_odometry_amd import native_ops
+
+    n = 64
+    assert native_ops.solve_tape_supported(2, m, n, False, 50)
+    from deep_attention_visual_odometry_amd import _native as N
+
+    sc = native_ops.scene_struct(None, None, m, n, False, 2, N.DAVA_RESIDUAL_SQUARED_REPROJECTION)
+    cfg = native_ops.solver_config(1e-4, 0.9, -1.0, 50, -1.0, 1000, True, N.DAVA_HESSIAN_COMPACT)
+    assert lib.dava_ba_solve_backward_workspace_bytes(sc, cfg) > 0
+
+
+def test_generic_fallback_check_sizes_the_first_iterations(monkeypatch):
+    """BFGSSolver._check_generic_fits refuses only what cannot fit even at the first iterations and warns
+    (does not refuse) when only the iteration cap would not fit."""
+    import warnings
+
+    import torch
+
+    from deep_attention_visual_odometry_amd.autograd_solvers import bfgs_solver as mod
+
+    monkeypatch.setattr(mod, "_free_device_bytes", lambda device: 192 * 2.0 ** 30)
+    s = mod.BFGSSolver(hessian_mode="dense").eval()
+    x = torch.zeros(64, 789, requires_grad=True)  # C3 pinhole, B = 64: 0.16 GB per dense matrix
+    with pytest.warns(RuntimeWarning, match="stop"):
+        s._check_generic_fits(x, 1000)  # 3 x 1000 matrices would not fit; the run still goes ahead
+    with warnings.catch_warnings():
+        warnings.simplefilter("error")
+        s._check_generic_fits(x, 100)  # fits outright
+    with pytest.raises(RuntimeError, match="first temporaries"):
+        s._check_generic_fits(torch.zeros(48, 15093, requires_grad=True), 100)
+    with pytest.raises(RuntimeError, match="return_second_last"):
+        mod.BFGSSolver()._check_generic_fits(torch.zeros(48, 15093), 100, second_last=True)

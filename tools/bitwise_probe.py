@@ -42,7 +42,7 @@ def main():
     res = {}
     for name, env in cases:
         out = os.path.join(tmp, name + ".npy")
-        e = dict(os.environ, **env)
+        e = dict(os.environ, DAVA_DEBUG_OVERRIDES="1", **env)  # the binding reads DAVA_<NAME> once, at load
         if args.lib:
             e["DAVA_LIB"] = args.lib
         code = CHILD % {"repo": REPO, "shape": shape, "k": args.k, "out": out}

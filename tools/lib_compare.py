@@ -44,7 +44,7 @@ def main():
         out = os.path.join(tmp, tag + ".npz")
         code = CHILD % dict(repo=REPO, batch=args.batch, m=args.views, n=args.points, dist=not args.no_distortion,
                             seed=args.seed, k=args.k, out=out)
-        subprocess.run([sys.executable, "-c", code], env=dict(os.environ, DAVA_LIB=os.path.abspath(lib)),
+        subprocess.run([sys.executable, "-c", code], env=dict(os.environ, DAVA_DEBUG_OVERRIDES="1", DAVA_LIB=os.path.abspath(lib)),
                        check=True, timeout=300)
         res[tag] = np.load(out)
     xa, xb = res["a"]["x"], res["b"]["x"]

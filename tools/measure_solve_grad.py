@@ -4,7 +4,7 @@ time and peak device memory of the two paths, one JSON line per case.
   fused    the recording solve (one launch, tape in HBM) + the adjoint kernel (one launch),
            csrc/bfgs_adjoint.hip -- the default for ReprojectionError / RayAngleError closures
   generic  the per-iteration loop with a dense (B, P, P) inverse Hessian per iteration kept in the
-           autograd graph (HIP VJP kernels per op) -- DAVA_GENERIC_BACKWARD=1
+           autograd graph (HIP VJP kernels per op) -- the GENERIC_BACKWARD override
 
 Forward and backward are timed separately (HIP events on torch's current stream, after one
 warm-up); "problems_per_s" is B / (forward + backward).  The adjoint's algorithmic HBM bytes
@@ -39,10 +39,9 @@ def run(shape, b, k, path, dev, repeats=2):
     m, n, dist = SHAPES[shape]
     s = make_scenes(b, m, n, distortion=dist, seed=7, drop=0.0 if dist else 0.1)
     truth = torch.tensor(s.truth, device=dev, dtype=torch.float32)
-    if path == "generic":
-        os.environ["DAVA_GENERIC_BACKWARD"] = "1"
-    else:
-        os.environ.pop("DAVA_GENERIC_BACKWARD", None)
+    from deep_attention_visual_odometry_amd import _native
+
+    _native.set_debug_override("GENERIC_BACKWARD", 1 if path == "generic" else -1)
     solver = BFGSSolver(iterations=k, error_threshold=-1.0, minimum_step=-1.0).eval()
     times = []
     for rep in range(repeats + 1):  # the first round is the warm-up
@@ -64,7 +63,7 @@ def run(shape, b, k, path, dev, repeats=2):
         peak = torch.cuda.max_memory_allocated(dev) - base
         if rep > 0:
             times.append((ev[0].elapsed_time(ev[1]), ev[1].elapsed_time(ev[2])))
-    os.environ.pop("DAVA_GENERIC_BACKWARD", None)
+    _native.set_debug_override("GENERIC_BACKWARD", -1)
     fwd = min(t[0] for t in times)
     bwd = min(t[1] for t in times)
     p = x0.shape[1]
