@@ -699,12 +699,51 @@ __device__ __forceinline__ void compact_products_fused(int P, int Pv, int nh, co
     consume(j, s0, w0);
   }
   // EF entries of this wave in flight: all loads issued before any is consumed
-  for (; j + (EF - 1) * NW < nh; j += EF * NW) {
-    f4v s[EF][GM], w[EF][GM];
+#ifndef DAVA_FUSED_PIPELINE
+#define DAVA_FUSED_PIPELINE 0
+#endif
+#ifndef DAVA_FUSED_PIPELINE_EF
+#define DAVA_FUSED_PIPELINE_EF 2
+#endif
+  if constexpr (DAVA_FUSED_PIPELINE && GM <= DAVA_FUSED_PIPELINE) {
+    // two register batches: the next batch's loads are issued before this batch is consumed, so a
+    // wave keeps EF entries in flight while it does the arithmetic (same entries, same order)
+    constexpr int EF = DAVA_FUSED_PIPELINE_EF;
+    constexpr int STEP = EF * NW;
+    auto full = [&](int jj) { return jj + (EF - 1) * NW < nh; };
+    if (full(j)) {
+      f4v sA[EF][GM], wA[EF][GM], sB[EF][GM], wB[EF][GM];
 #pragma unroll
-    for (int e = 0; e < EF; ++e) load(j + e * NW, s[e], w[e]);
+      for (int e = 0; e < EF; ++e) load(j + e * NW, sA[e], wA[e]);
+      for (;;) {
+        const bool nb = full(j + STEP);
+        if (nb) {
 #pragma unroll
-    for (int e = 0; e < EF; ++e) consume(j + e * NW, s[e], w[e]);
+          for (int e = 0; e < EF; ++e) load(j + STEP + e * NW, sB[e], wB[e]);
+        }
+#pragma unroll
+        for (int e = 0; e < EF; ++e) consume(j + e * NW, sA[e], wA[e]);
+        j += STEP;
+        if (!nb) break;
+        const bool na = full(j + STEP);
+        if (na) {
+#pragma unroll
+          for (int e = 0; e < EF; ++e) load(j + STEP + e * NW, sA[e], wA[e]);
+        }
+#pragma unroll
+        for (int e = 0; e < EF; ++e) consume(j + e * NW, sB[e], wB[e]);
+        j += STEP;
+        if (!na) break;
+      }
+    }
+  } else {
+    for (; j + (EF - 1) * NW < nh; j += EF * NW) {
+      f4v s[EF][GM], w[EF][GM];
+#pragma unroll
+      for (int e = 0; e < EF; ++e) load(j + e * NW, s[e], w[e]);
+#pragma unroll
+      for (int e = 0; e < EF; ++e) consume(j + e * NW, s[e], w[e]);
+    }
   }
   for (; j < nh; j += NW) {  // the rest, one entry in flight
     f4v s0[GM], w0[GM];

@@ -126,6 +126,18 @@ for _t in ("f32", "f64"):
         f"dava_wolfe_init_{_t}": (ctypes.c_int, [_c_i64, _c_i64, _vp, _vp, _vp, _vp, _vp, _vp]),
         f"dava_wolfe_propose_{_t}": (ctypes.c_int, [_c_i64, _vp, _vp, _vp]),
         f"dava_wolfe_update_{_t}": (ctypes.c_int, [_c_i64, _c_i32, _scalar, _scalar, _c_i32, _vp, _vp, _vp]),
+        # host-memory flavours (csrc/bfgs_host.hip): the same signatures without the stream
+        f"dava_cpu_bfgs_update_inverse_hessian_{_t}": (ctypes.c_int, [_c_i64, _c_i64] + [_vp] * 4),
+        f"dava_cpu_bfgs_update_inverse_hessian_backward_{_t}": (ctypes.c_int, [_c_i64, _c_i64] + [_vp] * 7),
+        f"dava_cpu_bfgs_initial_scale_{_t}": (ctypes.c_int, [_c_i64, _c_i64] + [_vp] * 3),
+        f"dava_cpu_bfgs_initial_scale_backward_{_t}": (ctypes.c_int, [_c_i64, _c_i64] + [_vp] * 5),
+        f"dava_cpu_bfgs_scale_matrix_{_t}": (ctypes.c_int, [_c_i64, _c_i64] + [_vp] * 3),
+        f"dava_cpu_bfgs_scale_matrix_backward_{_t}": (ctypes.c_int, [_c_i64, _c_i64] + [_vp] * 5),
+        f"dava_cpu_bfgs_search_direction_{_t}": (ctypes.c_int, [_c_i64, _c_i64] + [_vp] * 3),
+        f"dava_cpu_bfgs_search_direction_backward_{_t}": (ctypes.c_int, [_c_i64, _c_i64] + [_vp] * 5),
+        f"dava_cpu_wolfe_init_{_t}": (ctypes.c_int, [_c_i64, _c_i64] + [_vp] * 5),
+        f"dava_cpu_wolfe_propose_{_t}": (ctypes.c_int, [_c_i64, _vp, _vp]),
+        f"dava_cpu_wolfe_update_{_t}": (ctypes.c_int, [_c_i64, _c_i32, _scalar, _scalar, _c_i32, _vp, _vp]),
     })
 
 _lock = threading.Lock()
@@ -213,6 +225,13 @@ def check(status: int, what: str) -> None:
     if status != DAVA_OK:
         msg = load_library().dava_status_string(status).decode()
         raise RuntimeError(f"{what} failed: {msg} (status {status})")
+
+
+def require_host_or_device_tensor(t: torch.Tensor, what: str) -> None:
+    """The generic building blocks run on ROCm tensors (HIP kernels) and on CPU tensors (the library's
+    host flavours, csrc/bfgs_host.hip) -- chosen by the tensor's device, never as a fallback."""
+    if not isinstance(t, torch.Tensor) or t.device.type not in ("cuda", "cpu"):
+        raise RuntimeError(f"{what} must be a ROCm device or CPU tensor; got {getattr(t, 'device', type(t))}")
 
 
 def require_device_tensor(t: torch.Tensor, what: str) -> None:

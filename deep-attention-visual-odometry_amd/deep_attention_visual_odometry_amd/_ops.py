@@ -521,6 +521,125 @@ def _(state, flags, trial, c1, c2, strong):
     return None
 
 
+# ------------------------------------------------ the same building blocks on CPU tensors
+# The reference's solver runs wherever `parameters` live (bfgs_solver.py:94-117; BASELINE C1 is "BFGS on
+# PyTorch CPU").  These CPU kernels call the host C++ flavours of the same library (csrc/bfgs_host.hip,
+# dava_cpu_*): explicit dispatch on the tensor's device, never a fallback for device tensors (a ROCm
+# tensor still goes to the HIP kernels and raises without them).  The fused BA objectives stay GPU-only.
+
+def _cpu(name: str, t: Tensor, *args) -> None:
+    N.check(getattr(N.load_library(), f"dava_cpu_{name}_{_dt(t)}")(*args), f"dava_cpu_{name}")
+
+
+def _cpu_ptr(t: Optional[Tensor]):
+    return None if t is None else N.ptr(t)
+
+
+@bfgs_update_inverse_hessian.register_kernel("cpu")
+def _(h, s, y):
+    b, n = _square_batch(h)
+    _same(s, h, (b, n), "step")
+    _same(y, h, (b, n), "delta_gradient")
+    out = torch.empty_like(h)
+    _cpu("bfgs_update_inverse_hessian", h, b, n, N.ptr(h), N.ptr(s), N.ptr(y), N.ptr(out))
+    return out
+
+
+@bfgs_update_inverse_hessian_backward.register_kernel("cpu")
+def _(h, s, y, grad, need_h, need_s, need_y):
+    b, n = _square_batch(h)
+    _same(grad, h, (b, n, n), "grad")
+    gh = torch.empty_like(h) if need_h else _empty0(h)
+    gs = torch.empty_like(s) if need_s else _empty0(h)
+    gy = torch.empty_like(y) if need_y else _empty0(h)
+    _cpu("bfgs_update_inverse_hessian_backward", h, b, n, N.ptr(h), N.ptr(s), N.ptr(y), N.ptr(grad),
+         _cpu_ptr(gh if need_h else None), _cpu_ptr(gs if need_s else None), _cpu_ptr(gy if need_y else None))
+    return gh, gs, gy
+
+
+@bfgs_initial_scale.register_kernel("cpu")
+def _(s, y):
+    b, n = s.shape
+    _same(y, s, (b, n), "delta_gradient")
+    out = s.new_empty((b,))
+    _cpu("bfgs_initial_scale", s, b, n, N.ptr(s), N.ptr(y), N.ptr(out))
+    return out
+
+
+@bfgs_initial_scale_backward.register_kernel("cpu")
+def _(s, y, grad, need_s, need_y):
+    b, n = s.shape
+    _same(grad, s, (b,), "grad")
+    gs = torch.empty_like(s) if need_s else _empty0(s)
+    gy = torch.empty_like(y) if need_y else _empty0(s)
+    _cpu("bfgs_initial_scale_backward", s, b, n, N.ptr(s), N.ptr(y), N.ptr(grad), _cpu_ptr(gs if need_s else None),
+         _cpu_ptr(gy if need_y else None))
+    return gs, gy
+
+
+@bfgs_scale_matrix.register_kernel("cpu")
+def _(scale, h):
+    b, n = _square_batch(h)
+    _same(scale, h, (b,), "scale")
+    out = torch.empty_like(h)
+    _cpu("bfgs_scale_matrix", h, b, n, N.ptr(scale), N.ptr(h), N.ptr(out))
+    return out
+
+
+@bfgs_scale_matrix_backward.register_kernel("cpu")
+def _(scale, h, grad, need_scale, need_h):
+    b, n = _square_batch(h)
+    _same(grad, h, (b, n, n), "grad")
+    gsc = torch.empty_like(scale) if need_scale else _empty0(h)
+    gh = torch.empty_like(h) if need_h else _empty0(h)
+    _cpu("bfgs_scale_matrix_backward", h, b, n, N.ptr(scale), N.ptr(h), N.ptr(grad),
+         _cpu_ptr(gsc if need_scale else None), _cpu_ptr(gh if need_h else None))
+    return gsc, gh
+
+
+@bfgs_search_direction.register_kernel("cpu")
+def _(h, g):
+    b, n = _square_batch(h)
+    _same(g, h, (b, n), "gradient")
+    out = torch.empty_like(g)
+    _cpu("bfgs_search_direction", h, b, n, N.ptr(h), N.ptr(g), N.ptr(out))
+    return out
+
+
+@bfgs_search_direction_backward.register_kernel("cpu")
+def _(h, g, grad, need_h, need_g):
+    b, n = _square_batch(h)
+    _same(grad, h, (b, n), "grad")
+    gh = torch.empty_like(h) if need_h else _empty0(h)
+    gg = torch.empty_like(g) if need_g else _empty0(h)
+    _cpu("bfgs_search_direction_backward", h, b, n, N.ptr(h), N.ptr(g), N.ptr(grad), _cpu_ptr(gh if need_h else None),
+         _cpu_ptr(gg if need_g else None))
+    return gh, gg
+
+
+@wolfe_init.register_kernel("cpu")
+def _(direction, f0, g0):
+    b, n = direction.shape
+    _same(g0, direction, (b, n), "base_gradient")
+    _same(f0, direction, (b,), "base_error")
+    state = direction.new_empty((b, WOLFE_STATE_COLUMNS))
+    flags = direction.new_empty((b, WOLFE_FLAG_COLUMNS), dtype=torch.uint8)
+    _cpu("wolfe_init", direction, b, n, N.ptr(direction), N.ptr(f0), N.ptr(g0), N.ptr(state), N.ptr(flags))
+    return state, flags
+
+
+@wolfe_propose.register_kernel("cpu")
+def _(state, flags):
+    b = _check_wolfe(state, flags)
+    _cpu("wolfe_propose", state, b, N.ptr(state), N.ptr(flags))
+
+
+@wolfe_update.register_kernel("cpu")
+def _(state, flags, trial, c1, c2, strong):
+    b = _check_wolfe(state, flags)
+    _cpu("wolfe_update", state, b, int(trial), float(c1), float(c2), 1 if strong else 0, N.ptr(state), N.ptr(flags))
+
+
 # ------------------------------------------------ legacy L1 camera model evaluation
 
 @torch.library.custom_op("dava::l1_camera_evaluate", mutates_args=(), device_types=_CUDA)

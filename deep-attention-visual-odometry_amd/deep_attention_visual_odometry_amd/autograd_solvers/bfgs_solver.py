@@ -28,7 +28,10 @@ Training mode's ``return_second_last`` runs fused too (a problem stopped by the 
 keeps x before its last step); when the reference's scatter would have moved rows between problems
 (``native_ops.second_last_moves_rows``) the solve is redone by the generic loop, which reproduces it.
 
-Not supported (raises rather than silently falling back): CPU tensors.
+CPU tensors with an ordinary closure run the generic loop on the library's host flavours of the
+building blocks (csrc/bfgs_host.hip), as the reference runs wherever ``parameters`` live
+(``:94-117``).  The fused objectives (:class:`ReprojectionError`, :class:`RayAngleError`) are
+GPU-only and raise on CPU tensors; nothing ever falls back from the GPU to the CPU.
 """
 from typing import Callable, Optional
 
@@ -98,7 +101,9 @@ class BFGSSolver(Module):
     # ---- forward ----
     def forward(self, parameters: torch.Tensor,
                 error_function: Callable[[torch.Tensor, torch.Tensor], torch.Tensor]) -> torch.Tensor:
-        _native.require_device_tensor(parameters, "parameters")
+        if isinstance(error_function, ReprojectionError) or not isinstance(parameters, torch.Tensor) \
+                or parameters.device.type != "cpu":
+            _native.require_device_tensor(parameters, "parameters")  # the fused objectives are GPU-only
         if self.training:
             error_threshold, num_iterations = self.training_error_threshold, self.training_iterations
         else:

@@ -4,8 +4,9 @@
 Same signature, argument meaning, warning and return value.  The bracketing
 state machine (N&W algorithms 3.5/3.6 with bisection zoom, at most 1000
 trials, result = the upper bracket) runs in HIP kernels
-(``dava_wolfe_{init,propose,update}``); only the caller's ``error_function``
-and its derivative w.r.t. alpha are evaluated by PyTorch, on the device.
+(``dava_wolfe_{init,propose,update}``; on CPU tensors the library's host flavours
+``dava_cpu_wolfe_*``); only the caller's ``error_function`` and its derivative w.r.t.
+alpha are evaluated by PyTorch, where the tensors live.
 The host loop still asks "is any problem active?" once per trial, exactly
 where the reference synchronises (``wolfe_conditions.py:119-121``).
 
@@ -38,7 +39,7 @@ def line_search_wolfe_conditions(
             f"Line search conditions should satisfy 0 < c1 < c2 < 1. "
             f"Got c1={sufficient_decrease} and c2={curvature}"
         )
-    _native.require_device_tensor(parameters, "parameters")
+    _native.require_host_or_device_tensor(parameters, "parameters")
     parameters = parameters.detach()
     search_direction = search_direction.detach()
     base_error = base_error.detach()

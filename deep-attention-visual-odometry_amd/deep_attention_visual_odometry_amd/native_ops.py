@@ -210,7 +210,9 @@ def adjoint_lds_entries(batch: int, num_views: int, num_points: int, distortion:
 # differentiated through exactly like the reference (bfgs_solver.py:85, :134, :213-215).
 
 def _device_tensor(t: torch.Tensor, what: str) -> torch.Tensor:
-    N.require_device_tensor(t, what)
+    """A ROCm tensor (HIP kernels) or a CPU tensor (the library's host flavours): the operators dispatch
+    on the device."""
+    N.require_host_or_device_tensor(t, what)
     _dt(t)
     return t
 

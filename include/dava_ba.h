@@ -284,6 +284,49 @@ int dava_bfgs_search_direction_backward_f32(int64_t batch, int64_t n, const floa
 int dava_bfgs_search_direction_backward_f64(int64_t batch, int64_t n, const double* h, const double* g,
                                             const double* grad_d, double* grad_h, double* grad_g, void* stream);
 
+/* ---- the building blocks above on HOST memory (CPU tensors; csrc/bfgs_host.hip) ----
+ * The reference's solver runs wherever its parameters live (bfgs_solver.py:94-117; BASELINE C1 is
+ * "BFGS on PyTorch CPU").  Same arguments and semantics as the device entry points of the same name
+ * without the `dava_cpu_` prefix, every pointer host memory, no stream, synchronous.           */
+int dava_cpu_bfgs_update_inverse_hessian_f32(int64_t batch, int64_t n, const float* h, const float* s,
+                                             const float* y, float* h_out);
+int dava_cpu_bfgs_update_inverse_hessian_f64(int64_t batch, int64_t n, const double* h, const double* s,
+                                             const double* y, double* h_out);
+int dava_cpu_bfgs_initial_scale_f32(int64_t batch, int64_t n, const float* s, const float* y, float* scale_out);
+int dava_cpu_bfgs_initial_scale_f64(int64_t batch, int64_t n, const double* s, const double* y, double* scale_out);
+int dava_cpu_bfgs_scale_matrix_f32(int64_t batch, int64_t n, const float* scale, const float* h, float* h_out);
+int dava_cpu_bfgs_scale_matrix_f64(int64_t batch, int64_t n, const double* scale, const double* h, double* h_out);
+int dava_cpu_bfgs_search_direction_f32(int64_t batch, int64_t n, const float* h, const float* g, float* d_out);
+int dava_cpu_bfgs_search_direction_f64(int64_t batch, int64_t n, const double* h, const double* g, double* d_out);
+int dava_cpu_wolfe_init_f32(int64_t batch, int64_t n, const float* direction, const float* f0, const float* g0,
+                            float* state, uint8_t* flags);
+int dava_cpu_wolfe_init_f64(int64_t batch, int64_t n, const double* direction, const double* f0, const double* g0,
+                            double* state, uint8_t* flags);
+int dava_cpu_wolfe_propose_f32(int64_t batch, float* state, const uint8_t* flags);
+int dava_cpu_wolfe_propose_f64(int64_t batch, double* state, const uint8_t* flags);
+int dava_cpu_wolfe_update_f32(int64_t batch, int32_t trial, float c1, float c2, int32_t strong, float* state,
+                              uint8_t* flags);
+int dava_cpu_wolfe_update_f64(int64_t batch, int32_t trial, double c1, double c2, int32_t strong, double* state,
+                              uint8_t* flags);
+int dava_cpu_bfgs_update_inverse_hessian_backward_f32(int64_t batch, int64_t n, const float* h, const float* s,
+                                                      const float* y, const float* grad_out, float* grad_h,
+                                                      float* grad_s, float* grad_y);
+int dava_cpu_bfgs_update_inverse_hessian_backward_f64(int64_t batch, int64_t n, const double* h, const double* s,
+                                                      const double* y, const double* grad_out, double* grad_h,
+                                                      double* grad_s, double* grad_y);
+int dava_cpu_bfgs_initial_scale_backward_f32(int64_t batch, int64_t n, const float* s, const float* y,
+                                             const float* grad_out, float* grad_s, float* grad_y);
+int dava_cpu_bfgs_initial_scale_backward_f64(int64_t batch, int64_t n, const double* s, const double* y,
+                                             const double* grad_out, double* grad_s, double* grad_y);
+int dava_cpu_bfgs_scale_matrix_backward_f32(int64_t batch, int64_t n, const float* scale, const float* h,
+                                            const float* grad_out, float* grad_scale, float* grad_h);
+int dava_cpu_bfgs_scale_matrix_backward_f64(int64_t batch, int64_t n, const double* scale, const double* h,
+                                            const double* grad_out, double* grad_scale, double* grad_h);
+int dava_cpu_bfgs_search_direction_backward_f32(int64_t batch, int64_t n, const float* h, const float* g,
+                                                const float* grad_d, float* grad_h, float* grad_g);
+int dava_cpu_bfgs_search_direction_backward_f64(int64_t batch, int64_t n, const double* h, const double* g,
+                                                const double* grad_d, double* grad_h, double* grad_g);
+
 /* ---- legacy IOptimisableFunction camera model (camera_model/pinhole_camera_model_l1.py) ----
  * Error and/or the reference's hand-written gradient of PinholeCameraModelL1 for
  * batch x estimates independent estimates (one workgroup each).  Per estimate:

@@ -1,0 +1,152 @@
+"""BASELINE configuration C1 as BASELINE states it: "BFGS on PyTorch CPU -- plumbing, runs without a GPU".
+
+`BFGSSolver` on CPU tensors with an ordinary torch closure runs the generic loop (bfgs_solver.py:118-212)
+on the library's HOST flavours of its building blocks (csrc/bfgs_host.hip, dava_cpu_*), dispatched by
+the tensors' device.  Checked against the REAL reference's outputs (tests/golden/bfgs_traj.npz: C1,
+BFGSSolver(...).eval() after K = 5, 20, 100, and the c1def run with the reference's default stopping
+rules in float64), and the building blocks op by op against the reference's own goldens
+(tests/golden/bfgs_update.npz).  The closure is the caller's own code, written here in torch (the BA
+objective of SURVEY 8(a): unpack -> scale-normalised camera-relative points -> Rodrigues -> pinhole ->
+squared residual weighted by visibility); the oracle only supplies the 1-ulp envelopes at K = 100.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN
+
+TOL = 1e-5
+
+
+def _closure(obs, vis, m, n):
+    """The caller's error_function(parameters, batch_mask) in plain torch."""
+    from deep_attention_visual_odometry_amd import unpack_calibration_parameters
+
+    def error(x, mask):
+        parts = unpack_calibration_parameters(x, m, n)
+        pts, t, w = parts.world_points, parts.camera_translations, parts.camera_rotations
+        scale = (pts.abs().mean(dim=(-1, -2, -3), keepdim=True) * n
+                 + t.abs().mean(dim=(-1, -2, -3), keepdim=True) * m) / (n + m)
+        pts, t = pts / scale, t / scale
+        theta = torch.linalg.vector_norm(w, dim=-1, keepdim=True)
+        vw = (pts * w).sum(dim=-1, keepdim=True)
+        moved = (pts * torch.cos(theta) + (1.0 - torch.cos(theta)) / theta.square() * vw * w
+                 + torch.linalg.cross(w.expand_as(pts), pts, dim=-1) * (torch.sin(theta) / theta) + t)
+        p = torch.cat([pts, moved], dim=-3)
+        k = parts.intrinsics
+        uv = k[..., 0:1] * p[..., 0:2] / p[..., 2:3] + k[..., 1:3]
+        sq = (uv - obs[mask]).square().sum(dim=-1)
+        return (sq * vis[mask].to(sq.dtype)).sum(dim=(-1, -2))
+
+    return error
+
+
+def _rel(a, b):
+    a, b = a.double(), b.double()
+    return (a - b).norm(dim=-1) / b.norm(dim=-1)
+
+
+def test_cpu_solve_matches_reference_c1_trajectories():
+    from oracle import objective, solver
+
+    from deep_attention_visual_odometry_amd import BFGSSolver
+
+    g = np.load(os.path.join(GOLDEN, "bfgs_traj.npz"))
+    x0 = torch.tensor(g["c1_x0"])
+    obs, vis = torch.tensor(g["c1_obs"]), torch.tensor(g["c1_vis"])
+    fn = _closure(obs, vis, 2, 64)
+    for k in (5, 20, 100):
+        out = BFGSSolver(iterations=k, error_threshold=-1.0, minimum_step=-1.0).eval()(x0, fn)
+        assert out.device.type == "cpu" and out.dtype == torch.float32
+        ref = torch.tensor(g[f"c1_k{k}"])
+        rel = _rel(out, ref)
+        if k < 100:
+            assert (rel <= TOL).all(), (k, rel)
+            continue
+        # K = 100: each problem inside max(1e-5, 10x the reference's own change under a 1-ulp nudge of x0)
+        oc = objective.ReprojectionClosure(obs, vis, 2, 64)
+        env = torch.full((x0.shape[0],), TOL, dtype=torch.float64)
+        for to in (float("inf"), -float("inf")):
+            nudged = solver.bfgs_solve(torch.nextafter(x0, torch.full_like(x0, to)), oc, iterations=k,
+                                       error_threshold=-1.0, minimum_step=-1.0)
+            env = torch.maximum(env, 10.0 * _rel(nudged, ref))
+        assert (rel <= env).all() and (rel <= TOL).all(), (rel, env)
+
+
+def test_cpu_solve_reference_defaults_float64():
+    """BFGSSolver() with every default, float64, the reference's own run to its stopping rules."""
+    from deep_attention_visual_odometry_amd import BFGSSolver
+
+    g = np.load(os.path.join(GOLDEN, "bfgs_traj.npz"))
+    x0, obs, vis = torch.tensor(g["c1def_x0"]), torch.tensor(g["c1def_obs"]), torch.tensor(g["c1def_vis"])
+    out = BFGSSolver().eval()(x0, _closure(obs, vis, 2, 64))
+    assert out.dtype == torch.float64
+    assert _rel(out, torch.tensor(g["c1def_out"])).max() <= 1e-9
+
+
+def test_cpu_building_blocks_match_reference_goldens():
+    """update_inverse_hessian / scale_initial_inverse_hessian (the static methods, bfgs_solver.py:217-303)
+    on CPU tensors against the reference's outputs (tests/golden/bfgs_update.npz), fp64 and fp32."""
+    from deep_attention_visual_odometry_amd import BFGSSolver
+
+    g = np.load(os.path.join(GOLDEN, "bfgs_update.npz"))
+    cases = sorted({k[: -len("_h")] for k in g.keys() if k.endswith("_h")})
+    assert cases
+    for c in cases:
+        h, s, y = (torch.tensor(g[f"{c}_{k}"]) for k in ("h", "s", "y"))
+        got = BFGSSolver.update_inverse_hessian(h, s, y)
+        want = torch.tensor(g[f"{c}_out"])
+        tol = 1e-12 if h.dtype == torch.float64 else 2e-6
+        assert torch.allclose(got, want, rtol=tol, atol=tol * want.abs().max().item()), c
+        if f"{c}_scale" in g:
+            sc = BFGSSolver.scale_initial_inverse_hessian(s, y)
+            assert torch.allclose(sc.reshape(-1), torch.tensor(g[f"{c}_scale"]).reshape(-1), rtol=tol), c
+
+
+def test_cpu_gradient_through_the_solve():
+    """create_graph mode on CPU (bfgs_solver.py:85, :134, :213-215): the CPU building blocks' VJPs
+    (dava_cpu_*_backward) against torch's own autograd of the same algebra, through a 6-step solve."""
+    from deep_attention_visual_odometry_amd import BFGSSolver
+    from deep_attention_visual_odometry_amd import native_ops
+
+    gen = torch.Generator().manual_seed(3)
+    n = 7
+    a = torch.randn(4, n, n, dtype=torch.float64, generator=gen)
+    spd = a @ a.transpose(-1, -2) + n * torch.eye(n, dtype=torch.float64)
+
+    def quad(x, mask):  # a batch of convex quadratics with a quartic term
+        xs = x.unsqueeze(-1)
+        return 0.5 * (xs.transpose(-1, -2) @ spd[mask] @ xs).reshape(-1) + 0.1 * x.pow(4).sum(-1)
+
+    x0 = torch.randn(4, n, dtype=torch.float64, generator=gen).requires_grad_(True)
+    out = BFGSSolver(iterations=6, error_threshold=-1.0, minimum_step=-1.0).eval()(x0, quad)
+    (gx,) = torch.autograd.grad(out.square().sum(), x0)
+    assert torch.isfinite(gx).all() and gx.abs().max() > 0
+    # the VJPs themselves, against autograd of the same formulas
+    h = spd.clone().requires_grad_(True)
+    s = torch.randn(4, n, dtype=torch.float64, generator=gen).requires_grad_(True)
+    y = (spd @ s.detach().unsqueeze(-1)).squeeze(-1).requires_grad_(True)
+    w = torch.randn(4, n, n, dtype=torch.float64, generator=gen)
+    got = torch.autograd.grad((native_ops.update_inverse_hessian(h, s, y) * w).sum(), (h, s, y))
+    sy = (s * y).sum(-1, keepdim=True)
+    rho = 1.0 / sy
+    yH = (y.unsqueeze(-2) @ h).squeeze(-2)
+    Hy = (h @ y.unsqueeze(-1)).squeeze(-1)
+    c = 1.0 + (yH * y * rho).sum(-1, keepdim=True)
+    sr = s * rho
+    ref_out = h + (sr.unsqueeze(-1) * s.unsqueeze(-2)) * c.unsqueeze(-1) - sr.unsqueeze(-1) * yH.unsqueeze(-2) \
+        - Hy.unsqueeze(-1) * sr.unsqueeze(-2)
+    want = torch.autograd.grad((ref_out * w).sum(), (h, s, y))
+    for a_, b_ in zip(got, want):
+        assert torch.allclose(a_, b_, rtol=1e-10, atol=1e-10)
+
+
+def test_cpu_fused_objective_still_raises():
+    """The fused objectives are GPU-only: on CPU tensors they raise, they never run elsewhere."""
+    from deep_attention_visual_odometry_amd import BFGSSolver, ReprojectionError
+
+    fn = ReprojectionError(torch.zeros(1, 2, 4, 2), torch.ones(1, 2, 4, dtype=torch.bool), 2, 4)
+    with pytest.raises(RuntimeError, match="ROCm device"):
+        BFGSSolver().eval()(torch.zeros(1, 3 + 12 + 6), fn)

@@ -54,7 +54,7 @@ def _rel(a, b):
     return rel
 
 
-def _envelopes(x0, fn, ref, distortion=False, **kw):
+def _envelopes(x0, fn, ref, distortion=False, objective_of=None, **kw):
     """Per-problem 10x the oracle's own change under a 1-ulp nudge of x0, up or down (floor
     1e-5), for the whole parameter vector, for the intrinsics alone and (distortion) for the five
     Brown-Conrady coefficients alone.  Both directions: which side of a bifurcation a nudge lands
@@ -63,13 +63,18 @@ def _envelopes(x0, fn, ref, distortion=False, **kw):
     spread on it is 1e-4 .. 4e-3 at the headline shape, against ~5e-7 for the whole vector."""
     b = x0.shape[0]
     env, env_i, env_d = (torch.full((b,), TOL, dtype=torch.float64) for _ in range(3))
+    env_e = torch.full((b,), 1e-4, dtype=torch.float64)
     for to in (float("inf"), -float("inf")):
         nudged = solver.bfgs_solve(torch.nextafter(x0, torch.full_like(x0, to)), fn, **kw)
         env = torch.maximum(env, 10.0 * _rel(nudged, ref))
         env_i = torch.maximum(env_i, 10.0 * _rel(nudged[:, :3], ref[:, :3]))
         if distortion:
             env_d = torch.maximum(env_d, 10.0 * _rel(nudged[:, -5:], ref[:, -5:]))
-    return (env, env_i, env_d) if distortion else (env, env_i)
+        if objective_of is not None:  # the objective reached, relative: (E(nudged) - E(ref)) / E(ref)
+            e_ref, e_n = objective_of(ref), objective_of(nudged)
+            env_e = torch.maximum(env_e, torch.nan_to_num(10.0 * (e_n - e_ref).abs() / e_ref.abs(), nan=0.0))
+    out = (env, env_i, env_d) if distortion else (env, env_i)
+    return out + (env_e,) if objective_of is not None else out
 
 
 def _report(tag, rel, env=None, extra=None):
@@ -857,22 +862,28 @@ def _converged_check(tag, out, status, ref, rec, x0, fn, obs, vis, m, n, distort
     Every finite problem must stop at the same iteration for the same reason as the reference, and
     then its parameters are held to the fixed-K bar: per problem <= 1e-5 normwise and inside the
     reference's own 1-ulp envelope for the whole vector, the intrinsics and the five distortion
-    coefficients; the objective reached to 1e-3 relative (E is a small residual at the stop, ~1e-4,
-    so a 1e-6 relative move of x can move it by far more than 1e-6 of itself)."""
+    coefficients; the objective reached inside ITS 1-ulp envelope (10x the oracle's own relative change
+    of E under the nudge, floor 1e-4): E is a small residual at the stop (~1e-4), so a 1e-7 relative
+    move of x moves it by ~1e-3 of itself -- the measured C2 case, 3.6e-3 at 9.6e-7 in x."""
     finite = torch.isfinite(ref).all(dim=-1)
     assert torch.equal(torch.isfinite(out).all(dim=-1), finite)
+    def objective_of(x):
+        return objective.reprojection_error(x.double(), obs.double(), vis, m, n, distortion)
+
     if distortion:
-        env, env_i, env_d = _envelopes(x0, fn, ref, distortion=True)
+        env, env_i, env_d, env_e = _envelopes(x0, fn, ref, distortion=True, objective_of=objective_of)
     else:
-        (env, env_i), env_d = _envelopes(x0, fn, ref), torch.full((x0.shape[0],), float("inf"), dtype=torch.float64)
+        env, env_i, env_e = _envelopes(x0, fn, ref, objective_of=objective_of)
+        env_d = torch.full((x0.shape[0],), float("inf"), dtype=torch.float64)
     rel, rel_i, rel_d = _rel(out, ref), _rel(out[:, :3], ref[:, :3]), _rel(out[:, -5:], ref[:, -5:])
-    e_gpu = objective.reprojection_error(out.double(), obs.double(), vis, m, n, distortion)
-    e_ref = objective.reprojection_error(ref.double(), obs.double(), vis, m, n, distortion)
+    e_gpu, e_ref = objective_of(out), objective_of(ref)
     e_rel = ((e_gpu - e_ref).abs() / e_ref.abs())[finite]
+    env_e = env_e[finite]
     _report(tag, rel[finite], env[finite],
             {"intrinsics_max_rel": float(rel_i[finite].max()), "distortion_max_rel": float(rel_d[finite].max()),
              "distortion_max_rel_over_envelope": float((rel_d / env_d)[finite].max()),
-             "objective_max_rel": float(e_rel.max()), "steps_mean": float(status[finite, 0].double().mean()),
+             "objective_max_rel": float(e_rel.max()), "objective_max_rel_over_envelope": float((e_rel / env_e).max()),
+             "steps_mean": float(status[finite, 0].double().mean()),
              "stop_reasons": sorted(set(status[finite, 1].tolist())),
              "n_steps_differ": int((status[finite, 0] != rec.iterations[finite]).sum()),
              "n_reason_differs": int((status[finite, 1] != rec.reason[finite]).sum())})
@@ -881,7 +892,7 @@ def _converged_check(tag, out, status, ref, rec, x0, fn, obs, vis, m, n, distort
     assert (rel <= env).all() and (rel <= TOL).all(), rel
     assert (rel_i <= env_i).all(), rel_i
     assert (rel_d <= env_d).all(), (rel_d, env_d)
-    assert (e_rel <= 1e-3).all(), e_rel
+    assert (e_rel <= env_e).all(), (e_rel, env_e)
 
 
 def test_reference_golden_converged_distorted_parameters(device):
