@@ -379,40 +379,6 @@ __device__ __forceinline__ bool ba_eval(const Layout& L, const S* x, const S* d,
       }
     }
     S vg[7] = {0, 0, 0, 0, 0, 0, 0};  // gw_direct xyz, g_theta, g_t~ xyz
-#ifndef DAVA_ROTMAT
-#define DAVA_ROTMAT 0
-#endif
-    // ROTMAT: the view's Rodrigues rotation as a 3x3 matrix R = c I + A w w^T + B [w]x, formed once per
-    // view: p = R X~ + t~ (9 FMAs per pair instead of the vector form's 18), dE/dX~ = R^T G, and the
-    // view's rotation gradient from the per-thread sums Mg = sum_n G_n X~_n^T (9 FMAs per pair): every
-    // direct-w and theta term of the vector form is linear in Mg (sum (X~.w) G = Mg w, sum (G.w) X~ =
-    // Mg^T w, sum X~ x G = axial(Mg), sum G.X~ = tr Mg, sum (X~.w)(G.w) = w^T Mg w).  SLOPE:
-    // dp = R dX~ + Rdot X~ + dt~ with Rdot = dc I + dA w w^T + A (w dw^T + dw w^T) + B [dw]x + dB [w]x.
-    constexpr bool kRotMat = DAVA_ROTMAT;
-    S R[9], Rd[9], Mg[9];
-    if constexpr (kRotMat) {
-      const S ww[3] = {w0, w1, w2};
-#pragma unroll
-      for (int i = 0; i < 3; ++i)
-#pragma unroll
-        for (int j = 0; j < 3; ++j) {
-          R[3 * i + j] = vA * ww[i] * ww[j] + (i == j ? vc : S(0.0f));
-          Mg[3 * i + j] = 0.f;
-        }
-      R[1] -= vB * w2; R[2] += vB * w1; R[3] += vB * w2; R[5] -= vB * w0; R[6] -= vB * w1; R[7] += vB * w0;
-      if constexpr (SLOPE) {
-        const S dc = -vs * dth, dA = vAp * dth, dB = vTC * dth;
-        const S dd[3] = {dw0, dw1, dw2};
-#pragma unroll
-        for (int i = 0; i < 3; ++i)
-#pragma unroll
-          for (int j = 0; j < 3; ++j)
-            Rd[3 * i + j] = dA * ww[i] * ww[j] + vA * (ww[i] * dd[j] + dd[i] * ww[j]) + (i == j ? dc : S(0.0f));
-        Rd[1] -= vB * dw2 + dB * w2; Rd[2] += vB * dw1 + dB * w1; Rd[3] += vB * dw2 + dB * w2;
-        Rd[5] -= vB * dw0 + dB * w0; Rd[6] -= vB * dw1 + dB * w1; Rd[7] += vB * dw0 + dB * w0;
-      }
-    }
-    (void)R; (void)Rd; (void)Mg;
 
     // one (view m, point n) pair.  X / dX: the point's trial coordinates and direction;
     // q: its gradient, accumulated view after view (registers when PPT > 0, else loaded from
@@ -434,15 +400,6 @@ __device__ __forceinline__ bool ba_eval(const Layout& L, const S* x, const S* d,
       if (m == 0) {
         p0 = a0; p1 = a1; p2 = a2;
         if constexpr (SLOPE) { dp0 = da0; dp1 = da1; dp2 = da2; }
-      } else if constexpr (kRotMat) {
-        p0 = R[0] * a0 + R[1] * a1 + R[2] * a2 + tt0;
-        p1 = R[3] * a0 + R[4] * a1 + R[5] * a2 + tt1;
-        p2 = R[6] * a0 + R[7] * a1 + R[8] * a2 + tt2;
-        if constexpr (SLOPE) {
-          dp0 = (R[0] * da0 + R[1] * da1 + R[2] * da2) + (Rd[0] * a0 + Rd[1] * a1 + Rd[2] * a2) + dtt0;
-          dp1 = (R[3] * da0 + R[4] * da1 + R[5] * da2) + (Rd[3] * a0 + Rd[4] * a1 + Rd[5] * a2) + dtt1;
-          dp2 = (R[6] * da0 + R[7] * da1 + R[8] * da2) + (Rd[6] * a0 + Rd[7] * a1 + Rd[8] * a2) + dtt2;
-        }
       } else {
         vw = a0 * w0 + a1 * w1 + a2 * w2;
         c0 = w1 * a2 - w2 * a1;
@@ -551,14 +508,6 @@ __device__ __forceinline__ bool ba_eval(const Layout& L, const S* x, const S* d,
         S gx0, gx1, gx2;
         if (m == 0) {
           gx0 = G0; gx1 = G1; gx2 = G2;
-        } else if constexpr (kRotMat) {
-          gx0 = R[0] * G0 + R[3] * G1 + R[6] * G2;  // R^T G
-          gx1 = R[1] * G0 + R[4] * G1 + R[7] * G2;
-          gx2 = R[2] * G0 + R[5] * G1 + R[8] * G2;
-          Mg[0] += G0 * a0; Mg[1] += G0 * a1; Mg[2] += G0 * a2;
-          Mg[3] += G1 * a0; Mg[4] += G1 * a1; Mg[5] += G1 * a2;
-          Mg[6] += G2 * a0; Mg[7] += G2 * a1; Mg[8] += G2 * a2;
-          vg[4] += G0; vg[5] += G1; vg[6] += G2;  // dE/dt~
         } else {
           const S Gw = G0 * w0 + G1 * w1 + G2 * w2;
           const S Gv = G0 * a0 + G1 * a1 + G2 * a2;
@@ -606,45 +555,12 @@ __device__ __forceinline__ bool ba_eval(const Layout& L, const S* x, const S* d,
           return ScenePair{pf2{obs[2 * i0], obs[2 * i1]}, pf2{obs[2 * i0 + 1], obs[2 * i1 + 1]},
                            pf2{vis[i0] ? 1.0f : 0.0f, vis[i1] ? 1.0f : 0.0f}};
         };
-#ifndef DAVA_PACKED_ACC
-#define DAVA_PACKED_ACC 0
-#endif
-        // DAVA_PACKED_ACC: the sweep's sums kept as packed pairs (one v_pk_add per term instead of two
-        // scalar adds), folded into the scalar sums once per view: lane x sums point n0's terms, lane y
-        // point n1's.
-        struct PackSums {
-          pf2 e, sl, gin[8], vg[7], gsx, gdx, M[9];
-        } ps{};
-        auto fold = [&]() {
-          if constexpr (DAVA_PACKED_ACC) {
-            auto f = [](S& a, const pf2 t) {
-              a += t.x;
-              a += t.y;
-            };
-            f(e_loc, ps.e);
-            f(sl_loc, ps.sl);
-#pragma unroll
-            for (int k = 0; k < 8; ++k) f(gin[k], ps.gin[k]);
-#pragma unroll
-            for (int k = 0; k < 7; ++k) f(vg[k], ps.vg[k]);
-            f(gsx, ps.gsx);
-            f(gdx, ps.gdx);
-            if constexpr (kRotMat) {
-#pragma unroll
-              for (int k = 0; k < 9; ++k) f(Mg[k], ps.M[k]);
-            }
-          }
-        };
         auto pair2 = [&](const ScenePair& sp, const pf2 X0, const pf2 X1, const pf2 X2, const pf2 dX0,
                          const pf2 dX1, const pf2 dX2, pf2& q0, pf2& q1, pf2& q2) {
           const pf2 obu = sp.u, obv = sp.v, wgt = sp.w;
-          auto acc = [](S& a, pf2& packed, const pf2 t) {
-            if constexpr (DAVA_PACKED_ACC) {
-              packed += t;
-            } else {
-              a += t.x;
-              a += t.y;
-            }
+          auto acc = [](S& a, const pf2 t) {  // point n0's term, then n1's
+            a += t.x;
+            a += t.y;
           };
           const pf2 a0 = X0 * inv_s, a1 = X1 * inv_s, a2 = X2 * inv_s;
           pf2 da0 = 0.f, da1 = 0.f, da2 = 0.f;
@@ -658,15 +574,6 @@ __device__ __forceinline__ bool ba_eval(const Layout& L, const S* x, const S* d,
           if (m == 0) {
             p0 = a0; p1 = a1; p2 = a2;
             if constexpr (SLOPE) { dp0 = da0; dp1 = da1; dp2 = da2; }
-          } else if constexpr (kRotMat) {
-            p0 = R[0] * a0 + R[1] * a1 + R[2] * a2 + tt0;
-            p1 = R[3] * a0 + R[4] * a1 + R[5] * a2 + tt1;
-            p2 = R[6] * a0 + R[7] * a1 + R[8] * a2 + tt2;
-            if constexpr (SLOPE) {
-              dp0 = (R[0] * da0 + R[1] * da1 + R[2] * da2) + (Rd[0] * a0 + Rd[1] * a1 + Rd[2] * a2) + dtt0;
-              dp1 = (R[3] * da0 + R[4] * da1 + R[5] * da2) + (Rd[3] * a0 + Rd[4] * a1 + Rd[5] * a2) + dtt1;
-              dp2 = (R[6] * da0 + R[7] * da1 + R[8] * da2) + (Rd[6] * a0 + Rd[7] * a1 + Rd[8] * a2) + dtt2;
-            }
           } else {
             vw = a0 * w0 + a1 * w1 + a2 * w2;
             c0 = w1 * a2 - w2 * a1;
@@ -691,11 +598,7 @@ __device__ __forceinline__ bool ba_eval(const Layout& L, const S* x, const S* d,
           // z' == 0 nudge (distorted_camera_model.py:57), branch-free
           p2.x = p2.x + (p2.x == 0.0f ? z_nudge : -0.0f);
           p2.y = p2.y + (p2.y == 0.0f ? z_nudge : -0.0f);
-#ifndef DAVA_PACKED_RCP
-#define DAVA_PACKED_RCP 0
-#endif
-          // DAVA_PACKED_RCP: 1 / z by v_rcp_f32 (1 ulp) instead of the IEEE division sequence
-          const pf2 iz = DAVA_PACKED_RCP ? pf2{__builtin_amdgcn_rcpf(p2.x), __builtin_amdgcn_rcpf(p2.y)} : 1.0f / p2;
+          const pf2 iz = 1.0f / p2;
           const pf2 qx = p0 * iz, qy = p1 * iz;
           const pf2 ub = in.f * qx, vb = in.f * qy;
           pf2 u, vv, dub = 0.f, dvb = 0.f;
@@ -720,7 +623,7 @@ __device__ __forceinline__ bool ba_eval(const Layout& L, const S* x, const S* d,
             vv = vb + in.cy;
           }
           const pf2 ru = u - obu, rv = vv - obv;
-          acc(e_loc, ps.e, (ru * ru + rv * rv) * wgt);
+          acc(e_loc, (ru * ru + rv * rv) * wgt);
           if constexpr (SLOPE) {
             pf2 du = Juu * dub + Juv * dvb + din.cx;
             pf2 dv = Juv * dub + Jvv * dvb + din.cy;
@@ -731,38 +634,30 @@ __device__ __forceinline__ bool ba_eval(const Layout& L, const S* x, const S* d,
               dv += vb * (r2 * din.k1 + r4 * din.k2 + r4 * r2 * din.k3) + (r2 + 2.0f * vb * vb) * din.p1 +
                     2.0f * ub * vb * din.p2;
             }
-            acc(sl_loc, ps.sl, 2.0f * wgt * (ru * du + rv * dv));
+            acc(sl_loc, 2.0f * wgt * (ru * du + rv * dv));
           }
           if constexpr (GRAD) {
             const pf2 gu = 2.0f * wgt * ru, gv = 2.0f * wgt * rv;
-            acc(gin[1], ps.gin[1], gu);
-            acc(gin[2], ps.gin[2], gv);
+            acc(gin[1], gu);
+            acc(gin[2], gv);
             pf2 gub = gu, gvb = gv;
             if (L.distort) {
               gub = gu * Juu + gv * Juv;
               gvb = gu * Juv + gv * Jvv;
               const pf2 r4 = r2 * r2;
               const pf2 gr = gu * ub + gv * vb;
-              acc(gin[3], ps.gin[3], gr * r2);
-              acc(gin[4], ps.gin[4], gr * r4);
-              acc(gin[5], ps.gin[5], gr * r4 * r2);
-              acc(gin[6], ps.gin[6], gu * 2.0f * ub * vb + gv * (r2 + 2.0f * vb * vb));
-              acc(gin[7], ps.gin[7], gu * (r2 + 2.0f * ub * ub) + gv * 2.0f * ub * vb);
+              acc(gin[3], gr * r2);
+              acc(gin[4], gr * r4);
+              acc(gin[5], gr * r4 * r2);
+              acc(gin[6], gu * 2.0f * ub * vb + gv * (r2 + 2.0f * vb * vb));
+              acc(gin[7], gu * (r2 + 2.0f * ub * ub) + gv * 2.0f * ub * vb);
             }
-            acc(gin[0], ps.gin[0], gub * qx + gvb * qy);
+            acc(gin[0], gub * qx + gvb * qy);
             const pf2 fi = in.f * iz;
             const pf2 G0 = gub * fi, G1 = gvb * fi, G2 = -(gub * ub + gvb * vb) * iz;
             pf2 gx0, gx1, gx2;
             if (m == 0) {
               gx0 = G0; gx1 = G1; gx2 = G2;
-            } else if constexpr (kRotMat) {
-              gx0 = R[0] * G0 + R[3] * G1 + R[6] * G2;
-              gx1 = R[1] * G0 + R[4] * G1 + R[7] * G2;
-              gx2 = R[2] * G0 + R[5] * G1 + R[8] * G2;
-              acc(Mg[0], ps.M[0], G0 * a0); acc(Mg[1], ps.M[1], G0 * a1); acc(Mg[2], ps.M[2], G0 * a2);
-              acc(Mg[3], ps.M[3], G1 * a0); acc(Mg[4], ps.M[4], G1 * a1); acc(Mg[5], ps.M[5], G1 * a2);
-              acc(Mg[6], ps.M[6], G2 * a0); acc(Mg[7], ps.M[7], G2 * a1); acc(Mg[8], ps.M[8], G2 * a2);
-              acc(vg[4], ps.vg[4], G0); acc(vg[5], ps.vg[5], G1); acc(vg[6], ps.vg[6], G2);
             } else {
               const pf2 Gw = G0 * w0 + G1 * w1 + G2 * w2;
               const pf2 Gv = G0 * a0 + G1 * a1 + G2 * a2;
@@ -771,17 +666,17 @@ __device__ __forceinline__ bool ba_eval(const Layout& L, const S* x, const S* d,
               gx0 = vc * G0 + AGw * w0 + vB * (G1 * w2 - G2 * w1);
               gx1 = vc * G1 + AGw * w1 + vB * (G2 * w0 - G0 * w2);
               gx2 = vc * G2 + AGw * w2 + vB * (G0 * w1 - G1 * w0);
-              acc(vg[0], ps.vg[0], Avw * G0 + AGw * a0 + vB * (a1 * G2 - a2 * G1));
-              acc(vg[1], ps.vg[1], Avw * G1 + AGw * a1 + vB * (a2 * G0 - a0 * G2));
-              acc(vg[2], ps.vg[2], Avw * G2 + AGw * a2 + vB * (a0 * G1 - a1 * G0));
-              acc(vg[3], ps.vg[3], -vs * Gv + vAp * vw * Gw + vTC * Gx);
-              acc(vg[4], ps.vg[4], G0); acc(vg[5], ps.vg[5], G1); acc(vg[6], ps.vg[6], G2);
+              acc(vg[0], Avw * G0 + AGw * a0 + vB * (a1 * G2 - a2 * G1));
+              acc(vg[1], Avw * G1 + AGw * a1 + vB * (a2 * G0 - a0 * G2));
+              acc(vg[2], Avw * G2 + AGw * a2 + vB * (a0 * G1 - a1 * G0));
+              acc(vg[3], -vs * Gv + vAp * vw * Gw + vTC * Gx);
+              acc(vg[4], G0); acc(vg[5], G1); acc(vg[6], G2);
             }
             if (m == 0) { q0 = gx0; q1 = gx1; q2 = gx2; }
             else { q0 += gx0; q1 += gx1; q2 += gx2; }
             if (m == M - 1) {
-              acc(gsx, ps.gsx, q0 * X0 + q1 * X1 + q2 * X2);
-              if constexpr (DOT) acc(gdx, ps.gdx, q0 * dX0 + q1 * dX1 + q2 * dX2);
+              acc(gsx, q0 * X0 + q1 * X1 + q2 * X2);
+              if constexpr (DOT) acc(gdx, q0 * dX0 + q1 * dX1 + q2 * dX2);
             }
           }
         };
@@ -806,7 +701,6 @@ __device__ __forceinline__ bool ba_eval(const Layout& L, const S* x, const S* d,
             }
           }
         }
-        fold();
       }
       for (int n = n0; n < N; n += BLOCK) {
         const int ip = L.pt(n);
@@ -820,22 +714,6 @@ __device__ __forceinline__ bool ba_eval(const Layout& L, const S* x, const S* d,
         }
         pair(n, X0, X1, X2, dX0, dX1, dX2, q0, q1, q2);
         if constexpr (GRAD) { grad[ip] = q0; grad[ip + 1] = q1; grad[ip + 2] = q2; }
-      }
-    }
-    if constexpr (GRAD && kRotMat) {
-      if (m > 0) {  // the vector form's direct-w and theta sums, from this thread's Mg
-        const S Mw0 = Mg[0] * w0 + Mg[1] * w1 + Mg[2] * w2;
-        const S Mw1 = Mg[3] * w0 + Mg[4] * w1 + Mg[5] * w2;
-        const S Mw2 = Mg[6] * w0 + Mg[7] * w1 + Mg[8] * w2;
-        const S MTw0 = Mg[0] * w0 + Mg[3] * w1 + Mg[6] * w2;
-        const S MTw1 = Mg[1] * w0 + Mg[4] * w1 + Mg[7] * w2;
-        const S MTw2 = Mg[2] * w0 + Mg[5] * w1 + Mg[8] * w2;
-        const S ax0 = Mg[7] - Mg[5], ax1 = Mg[2] - Mg[6], ax2 = Mg[3] - Mg[1];  // sum X~ x G
-        vg[0] = vA * (Mw0 + MTw0) + vB * ax0;
-        vg[1] = vA * (Mw1 + MTw1) + vB * ax1;
-        vg[2] = vA * (Mw2 + MTw2) + vB * ax2;
-        vg[3] = -vs * (Mg[0] + Mg[4] + Mg[8]) + vAp * (w0 * Mw0 + w1 * Mw1 + w2 * Mw2) +
-                vTC * (w0 * ax0 + w1 * ax1 + w2 * ax2);
       }
     }
     if constexpr (GRAD) {

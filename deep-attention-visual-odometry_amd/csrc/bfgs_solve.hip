@@ -391,6 +391,11 @@ __device__ __forceinline__ void compact_products_wide(int P, int Pv, int nh, con
 #pragma unroll
       for (int u = 0; u < GT; ++u) {
         const int q = tid + u * BLOCK;
+        if (u < GT - 1 && (E == 1 || e < ne)) {  // groups 0 .. GT-2 lie inside the row for every thread
+          s4[e][u] = *reinterpret_cast<const f4v*>(S + (size_t)(j + e) * Pv + 4 * q);
+          w4[e][u] = *reinterpret_cast<const f4v*>(W + (size_t)(j + e) * Pv + 4 * q);
+          continue;
+        }
         s4[e][u] = w4[e][u] = z;
         if (e < ne && q < G) {
           s4[e][u] = *reinterpret_cast<const f4v*>(S + (size_t)(j + e) * Pv + 4 * q);
@@ -480,6 +485,11 @@ __device__ __forceinline__ float wide_direction(int P, int Pv, int nh, const flo
 #pragma unroll
       for (int u = 0; u < GT; ++u) {
         const int q = tid + u * BLOCK;
+        if (u < GT - 1 && (E == 1 || e < ne)) {  // groups 0 .. GT-2 lie inside the row for every thread
+          s4[e][u] = *reinterpret_cast<const f4v*>(S + (size_t)(j + e) * Pv + 4 * q);
+          w4[e][u] = *reinterpret_cast<const f4v*>(W + (size_t)(j + e) * Pv + 4 * q);
+          continue;
+        }
         s4[e][u] = w4[e][u] = z;
         if (e < ne && q < G) {
           s4[e][u] = *reinterpret_cast<const f4v*>(S + (size_t)(j + e) * Pv + 4 * q);
@@ -616,7 +626,7 @@ __device__ __forceinline__ void compact_products_fused(int P, int Pv, int nh, co
   bool ok[GM];
 #pragma unroll
   for (int m = 0; m < GM; ++m) {
-    ok[m] = lane + kWave * m < G;
+    ok[m] = m < GM - 1 || lane + kWave * m < G;  // (GM = ceil(G / 64): groups 0 .. GM-2 are full)
     pa[m] = f4v{0, 0, 0, 0};
     pb[m] = f4v{0, 0, 0, 0};
   }
@@ -698,52 +708,15 @@ __device__ __forceinline__ void compact_products_fused(int P, int Pv, int nh, co
     }
     consume(j, s0, w0);
   }
-  // EF entries of this wave in flight: all loads issued before any is consumed
-#ifndef DAVA_FUSED_PIPELINE
-#define DAVA_FUSED_PIPELINE 0
-#endif
-#ifndef DAVA_FUSED_PIPELINE_EF
-#define DAVA_FUSED_PIPELINE_EF 2
-#endif
-  if constexpr (DAVA_FUSED_PIPELINE && GM <= DAVA_FUSED_PIPELINE) {
-    // two register batches: the next batch's loads are issued before this batch is consumed, so a
-    // wave keeps EF entries in flight while it does the arithmetic (same entries, same order)
-    constexpr int EF = DAVA_FUSED_PIPELINE_EF;
-    constexpr int STEP = EF * NW;
-    auto full = [&](int jj) { return jj + (EF - 1) * NW < nh; };
-    if (full(j)) {
-      f4v sA[EF][GM], wA[EF][GM], sB[EF][GM], wB[EF][GM];
+  // EF entries of this wave in flight: all loads issued before any is consumed.  (Rejected, r04,
+  // profiles/r04_ab_variants_c2.log: two register batches, the next batch's loads issued before this
+  // one is consumed -- C2 -2..-8%.)
+  for (; j + (EF - 1) * NW < nh; j += EF * NW) {
+    f4v s[EF][GM], w[EF][GM];
 #pragma unroll
-      for (int e = 0; e < EF; ++e) load(j + e * NW, sA[e], wA[e]);
-      for (;;) {
-        const bool nb = full(j + STEP);
-        if (nb) {
+    for (int e = 0; e < EF; ++e) load(j + e * NW, s[e], w[e]);
 #pragma unroll
-          for (int e = 0; e < EF; ++e) load(j + STEP + e * NW, sB[e], wB[e]);
-        }
-#pragma unroll
-        for (int e = 0; e < EF; ++e) consume(j + e * NW, sA[e], wA[e]);
-        j += STEP;
-        if (!nb) break;
-        const bool na = full(j + STEP);
-        if (na) {
-#pragma unroll
-          for (int e = 0; e < EF; ++e) load(j + STEP + e * NW, sA[e], wA[e]);
-        }
-#pragma unroll
-        for (int e = 0; e < EF; ++e) consume(j + e * NW, sB[e], wB[e]);
-        j += STEP;
-        if (!na) break;
-      }
-    }
-  } else {
-    for (; j + (EF - 1) * NW < nh; j += EF * NW) {
-      f4v s[EF][GM], w[EF][GM];
-#pragma unroll
-      for (int e = 0; e < EF; ++e) load(j + e * NW, s[e], w[e]);
-#pragma unroll
-      for (int e = 0; e < EF; ++e) consume(j + e * NW, s[e], w[e]);
-    }
+    for (int e = 0; e < EF; ++e) consume(j + e * NW, s[e], w[e]);
   }
   for (; j < nh; j += NW) {  // the rest, one entry in flight
     f4v s0[GM], w0[GM];

@@ -6,6 +6,8 @@ f(alpha), phi'(alpha) = autograd w.r.t. alpha); the kernel evaluates the same tr
 forward-mode slope and the reverse-mode d . grad are compared with the oracle's.  Then the fused
 solve itself runs K = 1 .. --iterations and K = 100 against the oracle.
 usage: python tools/nonfinite_probe.py [--problem 4801] [--seed 7] [--iterations 3]
+       python tools/nonfinite_probe.py --batch 8 --problem 7 --seed 916 --drop 0.1 --iterations 3
+       (--batch > 0: generate that batch and take row --problem of it)
 """
 import argparse
 import json
@@ -28,13 +30,20 @@ def main():
     ap.add_argument("--problem", type=int, default=4801)
     ap.add_argument("--seed", type=int, default=7)
     ap.add_argument("--iterations", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=0)
+    ap.add_argument("--drop", type=float, default=0.0)
     args = ap.parse_args()
     from deep_attention_visual_odometry_amd import make_scenes, native_ops
     from oracle import objective, solver
 
     dev = torch.device("cuda", 0)
-    s = make_scenes(1, 4, 256, distortion=True, seed=args.seed, first_index=args.problem, drop=0.0)
-    x0, obs, vis = torch.tensor(s.initial), torch.tensor(s.observations), torch.tensor(s.visibility)
+    if args.batch > 0:
+        s = make_scenes(args.batch, 4, 256, distortion=True, seed=args.seed, drop=args.drop)
+        r = slice(args.problem, args.problem + 1)
+        x0, obs, vis = (torch.tensor(a)[r] for a in (s.initial, s.observations, s.visibility))
+    else:
+        s = make_scenes(1, 4, 256, distortion=True, seed=args.seed, first_index=args.problem, drop=args.drop)
+        x0, obs, vis = torch.tensor(s.initial), torch.tensor(s.observations), torch.tensor(s.visibility)
     fn = objective.ReprojectionClosure(obs, vis, 4, 256, True)
     log, traj = [], []
     solver.bfgs_solve(x0, fn, iterations=args.iterations, error_threshold=-1.0, minimum_step=-1.0,
