@@ -102,10 +102,6 @@ __host__ __device__ inline AdjointCarve carve_adjoint(int M, int N, int Pv, int 
 
 __device__ __forceinline__ f4a ldv(const float* p) { return *reinterpret_cast<const f4a*>(p); }
 __device__ __forceinline__ void stv(float* p, f4a v) { *reinterpret_cast<f4a*>(p) = v; }
-__device__ __forceinline__ float dot4(f4a a, f4a b) {
-  const f4a t = a * b;
-  return (t[0] + t[1]) + (t[2] + t[3]);
-}
 
 // One pass over entries j0 .. j1-1 with rows R1[j], R2[j] (Pv floats, rows Pv apart): per entry the
 // four dots d11 = R1.v1, d21 = R2.v1, d12 = R1.v2, d22 = R2.v2 (one transposed wave reduction),
@@ -147,24 +143,25 @@ __device__ __forceinline__ void pair_pass(int P, int Pv, int j0, int j1, const f
     load_from(R1 + (size_t)j * Pv, R2 + (size_t)j * Pv, r1, r2);
   };
   auto consume = [&](int j, const f4a (&r1)[GM], const f4a (&r2)[GM]) {
-    float d11 = 0.f, d21 = 0.f, d12 = 0.f, d22 = 0.f;
+    // packed 2-wide FMA chains for the dots, packed FMAs for the contributions (as the forward pass)
+    f2v d11 = {0.f, 0.f}, d21 = {0.f, 0.f}, d12 = {0.f, 0.f}, d22 = {0.f, 0.f};
 #pragma unroll
     for (int m = 0; m < GM; ++m) {
       const int q = lane + kWave * m;
       const f4a a = ok[m] ? ldv(v1 + 4 * q) : f4a{0, 0, 0, 0};
       const f4a c = ok[m] ? ldv(v2 + 4 * q) : f4a{0, 0, 0, 0};
-      d11 += dot4(r1[m], a);
-      d21 += dot4(r2[m], a);
-      d12 += dot4(r1[m], c);
-      d22 += dot4(r2[m], c);
+      d11 = pk_fma(r1[m].lo, a.lo, d11); d11 = pk_fma(r1[m].hi, a.hi, d11);
+      d21 = pk_fma(r2[m].lo, a.lo, d21); d21 = pk_fma(r2[m].hi, a.hi, d21);
+      d12 = pk_fma(r1[m].lo, c.lo, d12); d12 = pk_fma(r1[m].hi, c.hi, d12);
+      d22 = pk_fma(r2[m].lo, c.lo, d22); d22 = pk_fma(r2[m].hi, c.hi, d22);
     }
-    const float4 t = wave_sum4(d11, d21, d12, d22);
+    const float4 t = wave_sum4(d11.x + d11.y, d21.x + d21.y, d12.x + d12.y, d22.x + d22.y);
     float k1, k2, k3, k4;
     coef(j, t.x, t.y, t.z, t.w, k1, k2, k3, k4);
 #pragma unroll
     for (int m = 0; m < GM; ++m) {
-      pa[m] += k1 * r1[m] + k2 * r2[m];
-      pb[m] += k3 * r1[m] + k4 * r2[m];
+      pa[m] = pk_fma4(k2, r2[m], pk_fma4(k1, r1[m], pa[m]));
+      pb[m] = pk_fma4(k4, r2[m], pk_fma4(k3, r1[m], pb[m]));
     }
   };
   // EF entries of this wave in flight (kAdjInflight)
@@ -269,6 +266,8 @@ __device__ __forceinline__ void wide_pair_pass(int P, int Pv, int j0, int j1, co
 #pragma unroll
       for (int u = 0; u < GT; ++u) {
         const int q = tid + u * BLOCK;
+        // (every group exec-masked: the launch rounds GT up to an instantiated width, so unlike the
+        // forward's pass groups below GT - 1 may lie past the row)
         r1[e][u] = r2[e][u] = z;
         if (e < ne && q < G) {
           r1[e][u] = ldv(r1p + 4 * q);
@@ -276,17 +275,24 @@ __device__ __forceinline__ void wide_pair_pass(int P, int Pv, int j0, int j1, co
         }
       }
     }
+    // the four dots as packed 2-wide FMA chains (v_pk_fma_f32) and the contributions as packed FMAs,
+    // as the forward's history pass (wide_direction) forms them: 40% fewer VALU ops per entry than
+    // per-element products and horizontal adds
     float d[4 * E];
 #pragma unroll
     for (int e = 0; e < E; ++e) {
-      d[4 * e] = d[4 * e + 1] = d[4 * e + 2] = d[4 * e + 3] = 0.f;
+      f2v d11 = {0.f, 0.f}, d21 = {0.f, 0.f}, d12 = {0.f, 0.f}, d22 = {0.f, 0.f};
 #pragma unroll
       for (int u = 0; u < GT; ++u) {
-        d[4 * e] += dot4(r1[e][u], a[u]);
-        d[4 * e + 1] += dot4(r2[e][u], a[u]);
-        d[4 * e + 2] += dot4(r1[e][u], c[u]);
-        d[4 * e + 3] += dot4(r2[e][u], c[u]);
+        d11 = pk_fma(r1[e][u].lo, a[u].lo, d11); d11 = pk_fma(r1[e][u].hi, a[u].hi, d11);
+        d21 = pk_fma(r2[e][u].lo, a[u].lo, d21); d21 = pk_fma(r2[e][u].hi, a[u].hi, d21);
+        d12 = pk_fma(r1[e][u].lo, c[u].lo, d12); d12 = pk_fma(r1[e][u].hi, c[u].hi, d12);
+        d22 = pk_fma(r2[e][u].lo, c[u].lo, d22); d22 = pk_fma(r2[e][u].hi, c[u].hi, d22);
       }
+      d[4 * e] = d11.x + d11.y;
+      d[4 * e + 1] = d21.x + d21.y;
+      d[4 * e + 2] = d12.x + d12.y;
+      d[4 * e + 3] = d22.x + d22.y;
     }
     block_sum<4 * E, NW>(d, scratch, buf);
     buf ^= 1;
@@ -297,8 +303,8 @@ __device__ __forceinline__ void wide_pair_pass(int P, int Pv, int j0, int j1, co
         coef(j + e, d[4 * e], d[4 * e + 1], d[4 * e + 2], d[4 * e + 3], k1, k2, k3, k4);
 #pragma unroll
         for (int u = 0; u < GT; ++u) {
-          pa[u] += k1 * r1[e][u] + k2 * r2[e][u];
-          pb[u] += k3 * r1[e][u] + k4 * r2[e][u];
+          pa[u] = pk_fma4(k2, r2[e][u], pk_fma4(k1, r1[e][u], pa[u]));
+          pb[u] = pk_fma4(k4, r2[e][u], pk_fma4(k3, r1[e][u], pb[u]));
         }
       }
     }
@@ -408,26 +414,37 @@ __global__ __launch_bounds__(kWave * NW, GT > 0 ? 1 : kAdjLdsWpe) void bfgs_ba_a
   // mode nothing stands between the two)
   const float gamma = sc[3 * K];
 
+  // The per-step vector work goes float4-wide: thread t owns column groups t, t + BLOCK, ... (the row
+  // passes' ownership), so each element is touched by the same thread in every loop of a step.
+  auto each4 = [&](auto f) {
+    for (int q = tid; q < Pv / 4; q += BLOCK) f(4 * q);
+  };
+  auto below_p = [P](int i, f4a v) {  // elements >= P read as 0 (the scalar loops' i < P ? v : 0)
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      if (i + e >= P) v[e] = 0.f;
+    return v;
+  };
   for (int k = n - 1; k >= 0; --k) {
     const float alpha = sc[k];
     // ---- s_k = alpha d_k, x_{k+1} = x_k + s_k (alpha is a constant of the line search) ----
-    for (int i = tid; i < Pv; i += BLOCK) db[i] = alpha * (xb[i] + sbp[i]);
+    each4([&](int i) { stv(db + i, alpha * (ldv(xb + i) + ldv(sbp + i))); });
     if (k == 0) {
-      for (int i = tid; i < Pv; i += BLOCK) gk[i] = gbp[i] - db[i];  // d_0 = -g_0
+      each4([&](int i) { stv(gk + i, ldv(gbp + i) - ldv(db + i)); });  // d_0 = -g_0
     } else {
       const float* gk1 = Gr + (size_t)(k - 1) * Pv;
       const float* gkr = Gr + (size_t)k * Pv;
       const float* srow = S + (size_t)(k - 1) * Pv;
       const float* wrow = W + (size_t)(k - 1) * Pv;
       float* ak = Ar + (size_t)k * Pv;
-      for (int i = tid; i < Pv; i += BLOCK) {
-        const float g1 = i < P ? gkr[i] : 0.f, g0 = i < P ? gk1[i] : 0.f;
-        gv[i] = g1;
-        yv[i] = g1 - g0;
-        sv[i] = srow[i];
-        wv[i] = wrow[i];
-        akl[i] = anl[i] - db[i];  // d_k = -H_k g_k adds -dbar_k g_k^T to H_k's adjoint
-      }
+      each4([&](int i) {
+        const f4a g1 = below_p(i, ldv(gkr + i)), g0 = below_p(i, ldv(gk1 + i));
+        stv(gv + i, g1);
+        stv(yv + i, g1 - g0);
+        stv(sv + i, ldv(srow + i));
+        stv(wv + i, ldv(wrow + i));
+        stv(akl + i, ldv(anl + i) - ldv(db + i));  // d_k = -H_k g_k adds -dbar_k g_k^T to H_k's adjoint
+      });
       __syncthreads();
       const float rho = sc[K + k - 1], c = sc[2 * K + k - 1];
       // P1 = (A + A^T) s, P2 = (A + A^T) w over rows (a_j, g_j), j = k .. n-1
@@ -441,23 +458,30 @@ __global__ __launch_bounds__(kWave * NW, GT > 0 ? 1 : kAdjLdsWpe) void bfgs_ba_a
         pair_pass<GM>(P, Pv, k, n, Ar, Gr, sv, wv, 0.f, acoef, p1, p2, sp0, sp1, sp2, sp3, akl);
       }
       float r[7] = {0, 0, 0, 0, 0, 0, 0};
-      for (int i = tid; i < P; i += BLOCK) {
-        const float si = sv[i], wi = wv[i], yi = yv[i], di = db[i];
-        r[0] += si * p1[i]; r[1] += si * p2[i]; r[2] += yi * wi; r[3] += si * di; r[4] += wi * di;
-        r[5] += yi * yi; r[6] += si * yi;
-      }
+      each4([&](int i) {
+        const f4a s4 = ldv(sv + i), w4 = ldv(wv + i), y4 = ldv(yv + i), d4 = ldv(db + i), q1 = ldv(p1 + i),
+                  q2 = ldv(p2 + i);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          if (i + e < P) {
+            const float si = s4[e], wi = w4[e], yi = y4[e], di = d4[e];
+            r[0] += si * q1[e]; r[1] += si * q2[e]; r[2] += yi * wi; r[3] += si * di; r[4] += wi * di;
+            r[5] += yi * yi; r[6] += si * yi;
+          }
+        }
+      });
       block_sum<7, NW>(r, scratch, buf);
       buf ^= 1;
       const float sAs = 0.5f * r[0], sAw = r[1], yw = r[2], sd = r[3], wd = r[4], yy = r[5], t = r[6];
       const float cbar = rho * sAs;
       const float rhobar = c * sAs - sAw + cbar * yw;
       const float tbar = rho > 0.f ? -(rho * rho) * rhobar : 0.f;  // inverse_curvature backward
-      for (int i = tid; i < Pv; i += BLOCK) {
-        const float q1 = p1[i], q2 = p2[i];
-        wb[i] = -rho * q1 + (cbar * rho) * yv[i];
-        p2[i] = (cbar * rho) * wv[i] + tbar * sv[i];  // ybar, direct terms
-        sbp[i] = (c * rho) * q1 - rho * q2 + tbar * yv[i];
-      }
+      each4([&](int i) {
+        const f4a q1 = ldv(p1 + i), q2 = ldv(p2 + i), y4 = ldv(yv + i), w4 = ldv(wv + i), s4 = ldv(sv + i);
+        stv(wb + i, -rho * q1 + (cbar * rho) * y4);
+        stv(p2 + i, (cbar * rho) * w4 + tbar * s4);  // ybar, direct terms
+        stv(sbp + i, (c * rho) * q1 - rho * q2 + tbar * y4);
+      });
       __syncthreads();
       // H_{k-1} dbar and H_{k-1} wbar: one pass over history entries 0 .. k-2, plus gamma I
       if (k >= 2) {
@@ -472,26 +496,31 @@ __global__ __launch_bounds__(kWave * NW, GT > 0 ? 1 : kAdjLdsWpe) void bfgs_ba_a
         if constexpr (GVM) wide_pair_pass<GT, NW>(P, Pv, 0, k - 1, S, W, db, wb, gamma, hcoef, hd, hw, scratch, buf);
         else pair_pass<GM>(P, Pv, 0, k - 1, S, W, db, wb, gamma, hcoef, hd, hw, sp0, sp1, sp2, sp3, nullptr, lh, nlh);
       } else {
-        for (int i = tid; i < Pv; i += BLOCK) {
-          hd[i] = gamma * db[i];
-          hw[i] = gamma * wb[i];
-        }
+        each4([&](int i) {
+          stv(hd + i, gamma * ldv(db + i));
+          stv(hw + i, gamma * ldv(wb + i));
+        });
       }
       // H_k dbar = H_{k-1} dbar + entry k-1's rank-2 term;  gbar_k, a_k, a_{k-1}
       const float e1 = c * rho * sd - rho * wd, e2 = -rho * sd;
       float tr[1] = {0.f};
       const float* g0r = k == 1 ? Gr : nullptr;
-      for (int i = tid; i < Pv; i += BLOCK) {
-        const float ybar = p2[i] + hw[i];
-        const float hk = hd[i] + e1 * sv[i] + e2 * wv[i];
-        gk[i] = gbp[i] - hk + ybar;
-        gbp[i] = -ybar;
-        const float af = akl[i] + wb[i];
-        ak[i] = af;  // final a_k (read by the passes of steps < k)
-        anl[i] = -wb[i];
-        tr[0] += af * gv[i];
-        if (k == 1 && i < P) tr[0] -= wb[i] * g0r[i];  // a_0 = -wbar_1
-      }
+      each4([&](int i) {
+        const f4a ybar = ldv(p2 + i) + ldv(hw + i);  // (hw aliases gk: read before gk is written)
+        const f4a hk = ldv(hd + i) + e1 * ldv(sv + i) + e2 * ldv(wv + i);
+        const f4a w4 = ldv(wb + i), g4 = ldv(gv + i);
+        stv(gk + i, ldv(gbp + i) - hk + ybar);
+        stv(gbp + i, -ybar);
+        const f4a af = ldv(akl + i) + w4;
+        stv(ak + i, af);  // final a_k (read by the passes of steps < k)
+        stv(anl + i, -w4);
+        const f4a g0 = k == 1 ? ldv(g0r + i) : f4a{0, 0, 0, 0};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          tr[0] += af[e] * g4[e];
+          if (k == 1 && i + e < P) tr[0] -= w4[e] * g0[e];  // a_0 = -wbar_1
+        }
+      });
       block_sum<1, NW>(tr, scratch, buf);
       buf ^= 1;
       trace += tr[0];
@@ -502,15 +531,19 @@ __global__ __launch_bounds__(kWave * NW, GT > 0 ? 1 : kAdjLdsWpe) void bfgs_ba_a
         const float qbar = q >= 1e-4f ? trace : 0.f;  // clamp backward passes where input >= min
         const float tg = qbar / yyc;
         const float yybar = yy >= 1e-5f ? -qbar * q / yyc : 0.f;
-        for (int i = tid; i < Pv; i += BLOCK) {
-          const float extra = tg * sv[i] + 2.0f * yybar * yv[i];
-          sbp[i] += tg * yv[i];
-          gk[i] += extra;
-          gbp[i] -= extra;
-        }
+        each4([&](int i) {
+          const f4a y4 = ldv(yv + i);
+          const f4a extra = tg * ldv(sv + i) + 2.0f * yybar * y4;
+          stv(sbp + i, ldv(sbp + i) + tg * y4);
+          stv(gk + i, ldv(gk + i) + extra);
+          stv(gbp + i, ldv(gbp + i) - extra);
+        });
       }
     }
     // ---- g_k = dE/dx(x_k): xbar += Hess E gbar_k, obsbar += (d2E/dobs dx) gbar_k ----
+    // (the loops above own float4 groups, this one elements: gk's last writes -- the k = 0 line, the
+    // k = 1 gamma terms -- must land before another thread reads them)
+    __syncthreads();
     const float* xk = X + (size_t)k * Pv;
     for (int i = tid; i < Pv; i += BLOCK) {
       xd[i] = Dual(i < P ? xk[i] : 0.f, i < P ? gk[i] : 0.f);

@@ -138,17 +138,6 @@ __host__ __device__ inline LdsCarve carve_lds(int M, int N, int Pv, int kcap = 0
   return c;
 }
 
-typedef float f4v __attribute__((ext_vector_type(4)));
-typedef float f2v __attribute__((ext_vector_type(2)));
-
-// packed fp32 FMA (v_pk_fma_f32): a * b + c on two lanes of a float pair
-__device__ __forceinline__ f2v pk_fma(f2v a, f2v b, f2v c) { return __builtin_elementwise_fma(a, b, c); }
-// k * v + c on a float4 as two packed FMAs
-__device__ __forceinline__ f4v pk_fma4(float k, f4v v, f4v c) {
-  const f2v kk = {k, k};
-  const f2v lo = pk_fma(kk, v.lo, c.lo), hi = pk_fma(kk, v.hi, c.hi);
-  return f4v{lo.x, lo.y, hi.x, hi.y};
-}
 
 __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
 __device__ __forceinline__ void st4(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
@@ -594,9 +583,13 @@ __device__ __forceinline__ float wide_direction(int P, int Pv, int nh, const flo
 // latency-bound, few VALU ops per byte) drops to 0 so the partner's objective evaluation or
 // line-search step (VALU/LDS-latency-bound, the critical path) issues first: C3 +1.0%
 // (interleaved A/B, profiles/r01c_ab_wave_priority.log; levels 1..3 within noise of
-// each other).
+// each other).  Re-measured on the r04 kernel (profiles/r04_ab_c2_history.log): the drop still
+// pays for the short rows of four problems per CU (C2: without it -2%) but no longer for C3's
+// rows of four groups (without it +1.3%), so only rows of <= 2 groups per lane drop.
 constexpr int kBasePrio = 2;
 constexpr int kHistPrio = 0;
+template <int GM>
+constexpr bool kHistDropsPrio = GM <= 2;
 // EF: history entries in flight per wave (each holds 2 GM float4 rows in registers).  More
 // entries in flight = more bytes outstanding per wave, which is what the history stream of a
 // problem with few waves (or few problems per CU) is bound by.  (Interleaved A/B,
@@ -626,7 +619,10 @@ __device__ __forceinline__ void compact_products_fused(int P, int Pv, int nh, co
   bool ok[GM];
 #pragma unroll
   for (int m = 0; m < GM; ++m) {
-    ok[m] = m < GM - 1 || lane + kWave * m < G;  // (GM = ceil(G / 64): groups 0 .. GM-2 are full)
+    // (exec-masked for every group: telling the compiler that groups 0 .. GM-2 are full -- they are,
+    // GM = ceil(G / 64) -- dropped 14 instructions per 4-entry batch and cost C3 2.3%, C2 0.9%,
+    // interleaved A/B profiles/r04_ab_full_groups.log)
+    ok[m] = lane + kWave * m < G;
     pa[m] = f4v{0, 0, 0, 0};
     pb[m] = f4v{0, 0, 0, 0};
   }
@@ -694,7 +690,7 @@ __device__ __forceinline__ void compact_products_fused(int P, int Pv, int nh, co
       }
     }
   };
-  __builtin_amdgcn_s_setprio(kHistPrio);
+  if constexpr (kHistDropsPrio<GM>) __builtin_amdgcn_s_setprio(kHistPrio);
   int j = wave;
   for (const int nl = min(lcap, nh); j < nl; j += NW) {  // on-chip entries first (wave-uniform)
     f4v s0[GM], w0[GM];
@@ -723,7 +719,7 @@ __device__ __forceinline__ void compact_products_fused(int P, int Pv, int nh, co
     load(j, s0, w0);
     consume(j, s0, w0);
   }
-  __builtin_amdgcn_s_setprio(kBasePrio);
+  if constexpr (kHistDropsPrio<GM>) __builtin_amdgcn_s_setprio(kBasePrio);
   // deterministic cross-wave sum: ((w0 + w2) + (w1 + w3)) + gamma0 * (y | g)  (NW = 4),
   // (w0 + w1) + gamma0 * (y | g)  (NW = 2), w0 + gamma0 * (y | g)  (NW = 1).  With NW > 1 the last
   // adds are left to the caller's block-wide pass after its barrier (same operations, same order):

@@ -48,6 +48,18 @@ __device__ __forceinline__ float wave_sum<float>(float v) {
   return __uint_as_float(q[0]) + __uint_as_float(q[1]);  // xor 32
 }
 
+typedef float f4v __attribute__((ext_vector_type(4)));
+typedef float f2v __attribute__((ext_vector_type(2)));
+
+// packed fp32 FMA (v_pk_fma_f32): a * b + c on two lanes of a float pair
+__device__ __forceinline__ f2v pk_fma(f2v a, f2v b, f2v c) { return __builtin_elementwise_fma(a, b, c); }
+// k * v + c on a float4 as two packed FMAs
+__device__ __forceinline__ f4v pk_fma4(float k, f4v v, f4v c) {
+  const f2v kk = {k, k};
+  const f2v lo = pk_fma(kk, v.lo, c.lo), hi = pk_fma(kk, v.hi, c.hi);
+  return f4v{lo.x, lo.y, hi.x, hi.y};
+}
+
 __device__ __forceinline__ float lane_value(float v, int lane) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane));
 }
