@@ -995,9 +995,13 @@ def test_fused_second_last_gradient_multi_problem_batch(device):
     from deep_attention_visual_odometry_amd import BFGSSolver, ReprojectionError, native_ops
 
     x0, obs, vis, kw = _second_last_case(device, b=16)
-    kw = dict(kw, iterations=40)
-    _, _, st = native_ops.ba_solve(x0.to(device), obs.to(device), vis.to(device), 2, 64, False, hessian_mode=1,
-                                   want_status=True, return_second_last=True, **kw)
+    args = (x0.to(device), obs.to(device), vis.to(device), 2, 64, False)
+    # cap the iterations at the median stopping step: the batch then holds problems stopped by the
+    # minimum-step rule and problems stopped by the cap (uncapped, every problem of this scene stops by
+    # the rule within 2-6 steps)
+    _, _, st = native_ops.ba_solve(*args, hessian_mode=1, want_status=True, **kw)
+    kw = dict(kw, iterations=max(2, int(st[:, 0].float().median().item())))
+    _, _, st = native_ops.ba_solve(*args, hessian_mode=1, want_status=True, return_second_last=True, **kw)
     st = st.cpu()
     by_rule = (st[:, 1] == 2).nonzero().flatten().tolist()
     others = (st[:, 1] != 2).nonzero().flatten().tolist()
