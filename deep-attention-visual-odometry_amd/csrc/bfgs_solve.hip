@@ -621,7 +621,7 @@ __device__ __forceinline__ void compact_products_fused(int P, int Pv, int nh, co
   for (int m = 0; m < GM; ++m) {
     // (exec-masked for every group: telling the compiler that groups 0 .. GM-2 are full -- they are,
     // GM = ceil(G / 64) -- dropped 14 instructions per 4-entry batch and cost C3 2.3%, C2 0.9%,
-    // interleaved A/B profiles/r04_ab_full_groups.log)
+    // interleaved A/B profiles/r04_ab_full_groups_and_phase_scan.log)
     ok[m] = lane + kWave * m < G;
     pa[m] = f4v{0, 0, 0, 0};
     pb[m] = f4v{0, 0, 0, 0};
