@@ -380,6 +380,41 @@ __device__ __forceinline__ bool ba_eval(const Layout& L, const S* x, const S* d,
     }
     S vg[7] = {0, 0, 0, 0, 0, 0, 0};  // gw_direct xyz, g_theta, g_t~ xyz
 
+    // Packed sweeps (global-vector mode, squared objective): the view's Rodrigues rotation as a 3x3 matrix
+    // R = c I + A w w^T + B [w]x, formed once per view: p = R X~ + t~ (9 FMAs per pair instead of the
+    // vector form's 18), dE/dX~ = R^T G, and the view's rotation gradient from the per-thread sums
+    // Mg = sum_n G_n X~_n^T (9 FMAs per pair): every direct-w and theta term of the vector form is linear
+    // in Mg (sum (X~.w) G = Mg w, sum (G.w) X~ = Mg^T w, sum X~ x G = axial(Mg), sum G.X~ = tr Mg,
+    // sum (X~.w)(G.w) = w^T Mg w).  SLOPE: dp = R dX~ + Rdot X~ + dt~ with Rdot = dc I + dA w w^T +
+    // A (w dw^T + dw w^T) + B [dw]x + dB [w]x.  The same math in another rounding; the LDS-mode sweeps
+    // keep the vector form (there the matrix form measured C2 -3.5%, C3 -1.2%); C5 +1.9..2.4%
+    // (profiles/r04_ab_variants_c5.log, profiles/r04_ab_gv_rotmat.log, profiles/r04_ab_c5_dma_stream_rotmat.log).
+    constexpr bool kRotMat = PACK && std::is_same<S, float>::value && RES == DAVA_RESIDUAL_SQUARED_REPROJECTION;
+    S R[9], Rd[9], Mg[9];
+    if constexpr (kRotMat) {
+      const S ww[3] = {w0, w1, w2};
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+          R[3 * i + j] = vA * ww[i] * ww[j] + (i == j ? vc : S(0.0f));
+          Mg[3 * i + j] = 0.f;
+        }
+      R[1] -= vB * w2; R[2] += vB * w1; R[3] += vB * w2; R[5] -= vB * w0; R[6] -= vB * w1; R[7] += vB * w0;
+      if constexpr (SLOPE) {
+        const S dc = -vs * dth, dA = vAp * dth, dB = vTC * dth;
+        const S dd[3] = {dw0, dw1, dw2};
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+#pragma unroll
+          for (int j = 0; j < 3; ++j)
+            Rd[3 * i + j] = dA * ww[i] * ww[j] + vA * (ww[i] * dd[j] + dd[i] * ww[j]) + (i == j ? dc : S(0.0f));
+        Rd[1] -= vB * dw2 + dB * w2; Rd[2] += vB * dw1 + dB * w1; Rd[3] += vB * dw2 + dB * w2;
+        Rd[5] -= vB * dw0 + dB * w0; Rd[6] -= vB * dw1 + dB * w1; Rd[7] += vB * dw0 + dB * w0;
+      }
+    }
+    (void)R; (void)Rd; (void)Mg;
+
     // one (view m, point n) pair.  X / dX: the point's trial coordinates and direction;
     // q: its gradient, accumulated view after view (registers when PPT > 0, else loaded from
     // and stored back to `grad` by the caller below -- the same additions in the same order)
@@ -400,6 +435,15 @@ __device__ __forceinline__ bool ba_eval(const Layout& L, const S* x, const S* d,
       if (m == 0) {
         p0 = a0; p1 = a1; p2 = a2;
         if constexpr (SLOPE) { dp0 = da0; dp1 = da1; dp2 = da2; }
+      } else if constexpr (kRotMat) {
+        p0 = R[0] * a0 + R[1] * a1 + R[2] * a2 + tt0;
+        p1 = R[3] * a0 + R[4] * a1 + R[5] * a2 + tt1;
+        p2 = R[6] * a0 + R[7] * a1 + R[8] * a2 + tt2;
+        if constexpr (SLOPE) {
+          dp0 = (R[0] * da0 + R[1] * da1 + R[2] * da2) + (Rd[0] * a0 + Rd[1] * a1 + Rd[2] * a2) + dtt0;
+          dp1 = (R[3] * da0 + R[4] * da1 + R[5] * da2) + (Rd[3] * a0 + Rd[4] * a1 + Rd[5] * a2) + dtt1;
+          dp2 = (R[6] * da0 + R[7] * da1 + R[8] * da2) + (Rd[6] * a0 + Rd[7] * a1 + Rd[8] * a2) + dtt2;
+        }
       } else {
         vw = a0 * w0 + a1 * w1 + a2 * w2;
         c0 = w1 * a2 - w2 * a1;
@@ -508,6 +552,14 @@ __device__ __forceinline__ bool ba_eval(const Layout& L, const S* x, const S* d,
         S gx0, gx1, gx2;
         if (m == 0) {
           gx0 = G0; gx1 = G1; gx2 = G2;
+        } else if constexpr (kRotMat) {
+          gx0 = R[0] * G0 + R[3] * G1 + R[6] * G2;  // R^T G
+          gx1 = R[1] * G0 + R[4] * G1 + R[7] * G2;
+          gx2 = R[2] * G0 + R[5] * G1 + R[8] * G2;
+          Mg[0] += G0 * a0; Mg[1] += G0 * a1; Mg[2] += G0 * a2;
+          Mg[3] += G1 * a0; Mg[4] += G1 * a1; Mg[5] += G1 * a2;
+          Mg[6] += G2 * a0; Mg[7] += G2 * a1; Mg[8] += G2 * a2;
+          vg[4] += G0; vg[5] += G1; vg[6] += G2;  // dE/dt~
         } else {
           const S Gw = G0 * w0 + G1 * w1 + G2 * w2;
           const S Gv = G0 * a0 + G1 * a1 + G2 * a2;
@@ -574,6 +626,15 @@ __device__ __forceinline__ bool ba_eval(const Layout& L, const S* x, const S* d,
           if (m == 0) {
             p0 = a0; p1 = a1; p2 = a2;
             if constexpr (SLOPE) { dp0 = da0; dp1 = da1; dp2 = da2; }
+          } else if constexpr (kRotMat) {
+            p0 = R[0] * a0 + R[1] * a1 + R[2] * a2 + tt0;
+            p1 = R[3] * a0 + R[4] * a1 + R[5] * a2 + tt1;
+            p2 = R[6] * a0 + R[7] * a1 + R[8] * a2 + tt2;
+            if constexpr (SLOPE) {
+              dp0 = (R[0] * da0 + R[1] * da1 + R[2] * da2) + (Rd[0] * a0 + Rd[1] * a1 + Rd[2] * a2) + dtt0;
+              dp1 = (R[3] * da0 + R[4] * da1 + R[5] * da2) + (Rd[3] * a0 + Rd[4] * a1 + Rd[5] * a2) + dtt1;
+              dp2 = (R[6] * da0 + R[7] * da1 + R[8] * da2) + (Rd[6] * a0 + Rd[7] * a1 + Rd[8] * a2) + dtt2;
+            }
           } else {
             vw = a0 * w0 + a1 * w1 + a2 * w2;
             c0 = w1 * a2 - w2 * a1;
@@ -658,6 +719,14 @@ __device__ __forceinline__ bool ba_eval(const Layout& L, const S* x, const S* d,
             pf2 gx0, gx1, gx2;
             if (m == 0) {
               gx0 = G0; gx1 = G1; gx2 = G2;
+            } else if constexpr (kRotMat) {
+              gx0 = R[0] * G0 + R[3] * G1 + R[6] * G2;
+              gx1 = R[1] * G0 + R[4] * G1 + R[7] * G2;
+              gx2 = R[2] * G0 + R[5] * G1 + R[8] * G2;
+              acc(Mg[0], G0 * a0); acc(Mg[1], G0 * a1); acc(Mg[2], G0 * a2);
+              acc(Mg[3], G1 * a0); acc(Mg[4], G1 * a1); acc(Mg[5], G1 * a2);
+              acc(Mg[6], G2 * a0); acc(Mg[7], G2 * a1); acc(Mg[8], G2 * a2);
+              acc(vg[4], G0); acc(vg[5], G1); acc(vg[6], G2);
             } else {
               const pf2 Gw = G0 * w0 + G1 * w1 + G2 * w2;
               const pf2 Gv = G0 * a0 + G1 * a1 + G2 * a2;
@@ -714,6 +783,22 @@ __device__ __forceinline__ bool ba_eval(const Layout& L, const S* x, const S* d,
         }
         pair(n, X0, X1, X2, dX0, dX1, dX2, q0, q1, q2);
         if constexpr (GRAD) { grad[ip] = q0; grad[ip + 1] = q1; grad[ip + 2] = q2; }
+      }
+    }
+    if constexpr (GRAD && kRotMat) {
+      if (m > 0) {  // the vector form's direct-w and theta sums, from this thread's Mg
+        const S Mw0 = Mg[0] * w0 + Mg[1] * w1 + Mg[2] * w2;
+        const S Mw1 = Mg[3] * w0 + Mg[4] * w1 + Mg[5] * w2;
+        const S Mw2 = Mg[6] * w0 + Mg[7] * w1 + Mg[8] * w2;
+        const S MTw0 = Mg[0] * w0 + Mg[3] * w1 + Mg[6] * w2;
+        const S MTw1 = Mg[1] * w0 + Mg[4] * w1 + Mg[7] * w2;
+        const S MTw2 = Mg[2] * w0 + Mg[5] * w1 + Mg[8] * w2;
+        const S ax0 = Mg[7] - Mg[5], ax1 = Mg[2] - Mg[6], ax2 = Mg[3] - Mg[1];  // sum X~ x G
+        vg[0] = vA * (Mw0 + MTw0) + vB * ax0;
+        vg[1] = vA * (Mw1 + MTw1) + vB * ax1;
+        vg[2] = vA * (Mw2 + MTw2) + vB * ax2;
+        vg[3] = -vs * (Mg[0] + Mg[4] + Mg[8]) + vAp * (w0 * Mw0 + w1 * Mw1 + w2 * Mw2) +
+                vTC * (w0 * ax0 + w1 * ax1 + w2 * ax2);
       }
     }
     if constexpr (GRAD) {

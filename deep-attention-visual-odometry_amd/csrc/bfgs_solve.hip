@@ -444,12 +444,12 @@ __device__ __forceinline__ void compact_products_wide(int P, int Pv, int nh, con
 // the spills cost 14% with one entry and 19% with two.  Forming only H'g from the history and
 // H'y = H'g + d_prev: two entries per reduction, +0.5..0.9% at C5 but a different rounding that moved
 // a C2 problem 2.1e-5 from the oracle, profiles/r03_ab_hy_from_d.log.)
-template <int GT, int NW>
+template <int GT, int NW, bool STAGED = false>
 __device__ __forceinline__ float wide_direction(int P, int Pv, int nh, const float* __restrict__ S,
                                                 const float* __restrict__ W, float* hrho, float* hc, float gamma0,
                                                 const float* g, const float* gp, const float* s_cur, float* d,
                                                 float* s_row, float* w_row, float* scratch, int& buf, int entry,
-                                                float* tape_rho, float* tape_c) {
+                                                float* tape_rho, float* tape_c, float* stage = nullptr) {
   constexpr int BLOCK = kWave * NW;
   constexpr int E = GT <= 2 ? 2 : kGvEntries;
   const int tid = threadIdx.x;
@@ -465,7 +465,100 @@ __device__ __forceinline__ float wide_direction(int P, int Pv, int nh, const flo
       y[u] = gg[u] - *reinterpret_cast<const f4v*>(gp + 4 * q);
     }
   }
-  for (int j = 0; j < nh; j += E) {
+  // STAGED (XL images: stage = the dead LDS slots of d and the objective's gradient, 2 Pv floats): every
+  // entry's rows come HBM -> LDS by global_load_lds (no registers in flight), issued for entry j + 1 as
+  // soon as this thread has read entry j's groups back, so the copy runs under entry j's dots, block
+  // reduction and accumulation.  Each thread copies and reads back only its own float4 groups (the copy's
+  // lane-linear LDS layout is this pass's column ownership), so the staging buffer needs no barrier; the
+  // copy is issued from inline asm so that the compiler's wait accounting does not stall the LDS traffic
+  // of the reduction behind it, and its completion is waited for explicitly (vmcnt(0)) before the read.
+  // The same rows, dots and sums in the same order: bitwise the register path's result
+  // (profiles/r04_dma_stream_bitwise.log); C5 +4.5% (profiles/r04_ab_c5_dma_stream_rotmat.log).  M0 (the
+  // copy's LDS base) is saved and restored around each copy, so the compiler's view of it stays true.
+  constexpr bool staged = STAGED && E == 1;
+  if constexpr (staged) {
+    {
+      typedef __attribute__((address_space(3))) float lds_float;
+      const int wave = tid / kWave;
+      const unsigned stage_off = __builtin_amdgcn_readfirstlane(
+          (unsigned)(uintptr_t)((lds_float*)stage) + 16u * (unsigned)(wave * kWave));
+      const unsigned lane_off = 16u * (unsigned)(tid % kWave);  // this lane's 16 B within a wave's group
+      // copies address the rows as a wave-uniform 64-bit base (SGPRs) plus this thread's 32-bit byte
+      // offset 16 (tid + u BLOCK), so a copy costs one VGPR, not a 64-bit address per group
+      auto uniform_ptr64 = [](const float* p) {  // wave-uniform 64-bit address, in SGPRs
+        const unsigned long long v = (unsigned long long)(uintptr_t)p;
+        const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v);
+        const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
+        return ((unsigned long long)hi << 32) | lo;
+      };
+      const unsigned w_bytes = __builtin_amdgcn_readfirstlane(4u * (unsigned)Pv);
+      const unsigned voff = 16u * (unsigned)tid;  // one VGPR for every group: the group's step is in the base
+      auto copy = [&](int jj) {  // entry jj's S row -> stage[0, Pv), W row -> stage[Pv, 2 Pv), own groups
+#pragma unroll
+        for (int u = 0; u < GT; ++u) {
+          const int q = tid + u * BLOCK;
+          const unsigned long long srow_u = uniform_ptr64(S + (size_t)jj * Pv + 4 * u * BLOCK);
+          const unsigned long long wrow_u = uniform_ptr64(W + (size_t)jj * Pv + 4 * u * BLOCK);
+          const unsigned ds = __builtin_amdgcn_readfirstlane(stage_off + 16u * (unsigned)(u * BLOCK));
+          const unsigned dw = __builtin_amdgcn_readfirstlane(ds + w_bytes);
+          if (q < G) {
+            unsigned saved;
+            asm volatile(
+                "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\t"
+                "s_mov_b32 m0, %0"
+                : "=&s"(saved)
+                : "v"(voff), "s"(srow_u), "s"(ds)
+                : "memory");
+            asm volatile(
+                "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\t"
+                "s_mov_b32 m0, %0"
+                : "=&s"(saved)
+                : "v"(voff), "s"(wrow_u), "s"(dw)
+                : "memory");
+          }
+        }
+      };
+      (void)lane_off;
+      if (nh > 0) copy(0);
+      const float* st_s = stage + 4 * tid;  // this thread's groups: + 4 u BLOCK floats
+      const float* st_w = stage + Pv + 4 * tid;
+      for (int j = 0; j < nh; ++j) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this thread's copies of entry j have landed
+        f4v s4[GT], w4[GT];
+#pragma unroll
+        for (int u = 0; u < GT; ++u) {
+          const int q = tid + u * BLOCK;
+          s4[u] = w4[u] = z;
+          if (u < GT - 1 || q < G) {
+            s4[u] = *reinterpret_cast<const f4v*>(st_s + 4 * u * BLOCK);
+            w4[u] = *reinterpret_cast<const f4v*>(st_w + 4 * u * BLOCK);
+          }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // read back before the next copy overwrites it
+        if (j + 1 < nh) copy(j + 1);
+        f2v sy2 = {0.f, 0.f}, wy2 = {0.f, 0.f}, sg2 = {0.f, 0.f}, wg2 = {0.f, 0.f};
+#pragma unroll
+        for (int u = 0; u < GT; ++u) {
+          sy2 = pk_fma(s4[u].lo, y[u].lo, sy2); sy2 = pk_fma(s4[u].hi, y[u].hi, sy2);
+          wy2 = pk_fma(w4[u].lo, y[u].lo, wy2); wy2 = pk_fma(w4[u].hi, y[u].hi, wy2);
+          sg2 = pk_fma(s4[u].lo, gg[u].lo, sg2); sg2 = pk_fma(s4[u].hi, gg[u].hi, sg2);
+          wg2 = pk_fma(w4[u].lo, gg[u].lo, wg2); wg2 = pk_fma(w4[u].hi, gg[u].hi, wg2);
+        }
+        float dd[4] = {sy2.x + sy2.y, wy2.x + wy2.y, sg2.x + sg2.y, wg2.x + wg2.y};
+        block_sum<4, NW>(dd, scratch, buf);
+        buf ^= 1;
+        const float rho = hrho[j], cr = hc[j] * rho;
+        const float ay = fmaf(cr, dd[0], -(rho * dd[1])), by = -rho * dd[0];
+        const float ag = fmaf(cr, dd[2], -(rho * dd[3])), bg = -rho * dd[2];
+#pragma unroll
+        for (int u = 0; u < GT; ++u) {
+          pa[u] = pk_fma4(by, w4[u], pk_fma4(ay, s4[u], pa[u]));
+          pb[u] = pk_fma4(bg, w4[u], pk_fma4(ag, s4[u], pb[u]));
+        }
+      }
+    }
+  }
+  for (int j = 0; j < (staged ? 0 : nh); j += E) {  // (the register path)
     const int ne = min(E, nh - j);  // uniform
     f4v s4[E][GT], w4[E][GT];
     float dd[4 * E];
@@ -966,13 +1059,13 @@ __global__ __launch_bounds__(kWave * NW, kSolveWavesPerEU) void bfgs_ba_solve_ke
               const bool fuse = wide_history_pass(Pv, a.kcap, GV) && k - 1 < a.kcap;
               if (fuse) {
                 tail_done = true;
-                if (GT <= 1) dg = wide_direction<1, NW>(P, Pv, nh, SH, WH, hrho, hc, gamma0, g, gp, s_cur, d, srow, wrow, scratch, buf, k - 1, tr, tcp);
-                else if (GT == 2) dg = wide_direction<2, NW>(P, Pv, nh, SH, WH, hrho, hc, gamma0, g, gp, s_cur, d, srow, wrow, scratch, buf, k - 1, tr, tcp);
-                else if (GT == 3) dg = wide_direction<3, NW>(P, Pv, nh, SH, WH, hrho, hc, gamma0, g, gp, s_cur, d, srow, wrow, scratch, buf, k - 1, tr, tcp);
-                else if (GT == 4) dg = wide_direction<4, NW>(P, Pv, nh, SH, WH, hrho, hc, gamma0, g, gp, s_cur, d, srow, wrow, scratch, buf, k - 1, tr, tcp);
-                else if (GT == 5) dg = wide_direction<5, NW>(P, Pv, nh, SH, WH, hrho, hc, gamma0, g, gp, s_cur, d, srow, wrow, scratch, buf, k - 1, tr, tcp);
-                else if (GT == 6) dg = wide_direction<6, NW>(P, Pv, nh, SH, WH, hrho, hc, gamma0, g, gp, s_cur, d, srow, wrow, scratch, buf, k - 1, tr, tcp);
-                else dg = wide_direction<7, NW>(P, Pv, nh, SH, WH, hrho, hc, gamma0, g, gp, s_cur, d, srow, wrow, scratch, buf, k - 1, tr, tcp);
+                if (GT <= 1) dg = wide_direction<1, NW, XL>(P, Pv, nh, SH, WH, hrho, hc, gamma0, g, gp, s_cur, d, srow, wrow, scratch, buf, k - 1, tr, tcp, XL ? lds + cv.d : nullptr);
+                else if (GT == 2) dg = wide_direction<2, NW, XL>(P, Pv, nh, SH, WH, hrho, hc, gamma0, g, gp, s_cur, d, srow, wrow, scratch, buf, k - 1, tr, tcp, XL ? lds + cv.d : nullptr);
+                else if (GT == 3) dg = wide_direction<3, NW, XL>(P, Pv, nh, SH, WH, hrho, hc, gamma0, g, gp, s_cur, d, srow, wrow, scratch, buf, k - 1, tr, tcp, XL ? lds + cv.d : nullptr);
+                else if (GT == 4) dg = wide_direction<4, NW, XL>(P, Pv, nh, SH, WH, hrho, hc, gamma0, g, gp, s_cur, d, srow, wrow, scratch, buf, k - 1, tr, tcp, XL ? lds + cv.d : nullptr);
+                else if (GT == 5) dg = wide_direction<5, NW, XL>(P, Pv, nh, SH, WH, hrho, hc, gamma0, g, gp, s_cur, d, srow, wrow, scratch, buf, k - 1, tr, tcp, XL ? lds + cv.d : nullptr);
+                else if (GT == 6) dg = wide_direction<6, NW, XL>(P, Pv, nh, SH, WH, hrho, hc, gamma0, g, gp, s_cur, d, srow, wrow, scratch, buf, k - 1, tr, tcp, XL ? lds + cv.d : nullptr);
+                else dg = wide_direction<7, NW, XL>(P, Pv, nh, SH, WH, hrho, hc, gamma0, g, gp, s_cur, d, srow, wrow, scratch, buf, k - 1, tr, tcp, XL ? lds + cv.d : nullptr);
               } else if (!wide_history_pass(Pv, a.kcap, GV))
                 compact_products<GV ? 8 : 1, NW>(P, Pv, nh, SH, WH, hcoef, hrho, hc, gamma0, g, gp, hy_new, hg);
               else if (GT <= 1) compact_products_wide<1, NW>(P, Pv, nh, SH, WH, hrho, hc, gamma0, g, gp, hy_new, hg, scratch, buf);
