@@ -240,7 +240,7 @@ template <int GT, int NW, class Coef>
 __device__ __forceinline__ void wide_pair_pass(int P, int Pv, int j0, int j1, const float* __restrict__ R1,
                                                const float* __restrict__ R2, const float* v1, const float* v2,
                                                float base, Coef coef, float* out1, float* out2, float* scratch,
-                                               int& buf, const float* R1_j0 = nullptr) {
+                                               int& buf, const float* R1_j0 = nullptr, float* stage = nullptr) {
   constexpr int BLOCK = kWave * NW;
   constexpr int E = GT * NW <= 32 ? 2 : 1;  // two entries per reduction while the rows fit the registers
   const int tid = threadIdx.x;
@@ -256,7 +256,92 @@ __device__ __forceinline__ void wide_pair_pass(int P, int Pv, int j0, int j1, co
       c[u] = ldv(v2 + 4 * q);
     }
   }
-  for (int j = j0; j < j1; j += E) {
+  // stage (the HVP's dual gradient vector in LDS, dead during the passes: 2 Pv floats, one entry): the
+  // rows come HBM -> LDS by global_load_lds one entry ahead, each thread copying and reading back only
+  // its own column groups, as the forward's GV history pass does (bfgs_solve.hip, wide_direction).
+  // The same rows in the same order: bitwise the register path.
+  bool staged = false;
+  if constexpr (E == 1) {
+    if (stage != nullptr && j1 > j0) {
+      staged = true;
+      typedef __attribute__((address_space(3))) float lds_float;
+      const int wave = tid / kWave;
+      const unsigned stage_off = __builtin_amdgcn_readfirstlane(
+          (unsigned)(uintptr_t)((lds_float*)stage) + 16u * (unsigned)(wave * kWave));
+      const unsigned r2_bytes = __builtin_amdgcn_readfirstlane(4u * (unsigned)Pv);
+      const unsigned voff = 16u * (unsigned)tid;
+      auto uniform_ptr64 = [](const float* p) {
+        const unsigned long long v = (unsigned long long)(uintptr_t)p;
+        const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v);
+        const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
+        return ((unsigned long long)hi << 32) | lo;
+      };
+      auto copy = [&](int jj) {
+        const float* r1p = (R1_j0 && jj == j0) ? R1_j0 : R1 + (size_t)jj * Pv;
+        const float* r2p = R2 + (size_t)jj * Pv;
+#pragma unroll
+        for (int u = 0; u < GT; ++u) {
+          const int q = tid + u * BLOCK;
+          const unsigned long long b1 = uniform_ptr64(r1p + 4 * u * BLOCK);
+          const unsigned long long b2 = uniform_ptr64(r2p + 4 * u * BLOCK);
+          const unsigned d1 = __builtin_amdgcn_readfirstlane(stage_off + 16u * (unsigned)(u * BLOCK));
+          const unsigned d2 = __builtin_amdgcn_readfirstlane(d1 + r2_bytes);
+          if (q < G) {
+            unsigned saved;
+            asm volatile(
+                "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\t"
+                "s_mov_b32 m0, %0"
+                : "=&s"(saved)
+                : "v"(voff), "s"(b1), "s"(d1)
+                : "memory");
+            asm volatile(
+                "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\t"
+                "s_mov_b32 m0, %0"
+                : "=&s"(saved)
+                : "v"(voff), "s"(b2), "s"(d2)
+                : "memory");
+          }
+        }
+      };
+      copy(j0);
+      const float* st1 = stage + 4 * tid;
+      const float* st2 = stage + Pv + 4 * tid;
+      for (int j = j0; j < j1; ++j) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this thread's copies of entry j have landed
+        f4a r1[GT], r2[GT];
+#pragma unroll
+        for (int u = 0; u < GT; ++u) {
+          const int q = tid + u * BLOCK;
+          r1[u] = r2[u] = z;
+          if (q < G) {
+            r1[u] = ldv(st1 + 4 * u * BLOCK);
+            r2[u] = ldv(st2 + 4 * u * BLOCK);
+          }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // read back before the next copy overwrites it
+        if (j + 1 < j1) copy(j + 1);
+        f2v d11 = {0.f, 0.f}, d21 = {0.f, 0.f}, d12 = {0.f, 0.f}, d22 = {0.f, 0.f};
+#pragma unroll
+        for (int u = 0; u < GT; ++u) {
+          d11 = pk_fma(r1[u].lo, a[u].lo, d11); d11 = pk_fma(r1[u].hi, a[u].hi, d11);
+          d21 = pk_fma(r2[u].lo, a[u].lo, d21); d21 = pk_fma(r2[u].hi, a[u].hi, d21);
+          d12 = pk_fma(r1[u].lo, c[u].lo, d12); d12 = pk_fma(r1[u].hi, c[u].hi, d12);
+          d22 = pk_fma(r2[u].lo, c[u].lo, d22); d22 = pk_fma(r2[u].hi, c[u].hi, d22);
+        }
+        float d[4] = {d11.x + d11.y, d21.x + d21.y, d12.x + d12.y, d22.x + d22.y};
+        block_sum<4, NW, true>(d, scratch, buf);
+        buf ^= 1;
+        float k1, k2, k3, k4;
+        coef(j, d[0], d[1], d[2], d[3], k1, k2, k3, k4);
+#pragma unroll
+        for (int u = 0; u < GT; ++u) {
+          pa[u] = pk_fma4(k2, r2[u], pk_fma4(k1, r1[u], pa[u]));
+          pb[u] = pk_fma4(k4, r2[u], pk_fma4(k3, r1[u], pb[u]));
+        }
+      }
+    }
+  }
+  for (int j = j0; j < (staged ? j0 : j1); j += E) {  // (the register path)
     const int ne = min(E, j1 - j);  // uniform
     f4a r1[E][GT], r2[E][GT];
 #pragma unroll
@@ -367,6 +452,9 @@ __global__ __launch_bounds__(kWave * NW, GT > 0 ? 1 : kAdjLdsWpe) void bfgs_ba_a
   float* sc = lds + cv.sc;
   Dual* xd = reinterpret_cast<Dual*>(vb + cv.xd);
   Dual* gd = reinterpret_cast<Dual*>((GVM && a.gd_lds ? lds : vb) + cv.gd);
+  // GV passes: the rows staged through the dual gradient vector's LDS slots (dead until the HVP)
+  // (C5 adjoint 85.8 -> 79.7 ms, interleaved, profiles/r04_ab_adjoint_staged_c5.log)
+  float* stage = GVM && a.gd_lds ? lds + cv.gd : nullptr;
   Dual* views = reinterpret_cast<Dual*>(lds + cv.views);
   Dual* vpart = reinterpret_cast<Dual*>(lds + cv.vpart);
   const float* obs = GVM ? a.obs + (size_t)b * 2 * MN : lds + cv.obs;
@@ -453,7 +541,7 @@ __global__ __launch_bounds__(kWave * NW, GT > 0 ? 1 : kAdjLdsWpe) void bfgs_ba_a
         k1 = gs; k2 = as; k3 = gw; k4 = aw;
       };
       if constexpr (GVM) {
-        wide_pair_pass<GT, NW>(P, Pv, k, n, Ar, Gr, sv, wv, 0.f, acoef, p1, p2, scratch, buf, akl);
+        wide_pair_pass<GT, NW>(P, Pv, k, n, Ar, Gr, sv, wv, 0.f, acoef, p1, p2, scratch, buf, akl, stage);
       } else {
         pair_pass<GM>(P, Pv, k, n, Ar, Gr, sv, wv, 0.f, acoef, p1, p2, sp0, sp1, sp2, sp3, akl);
       }
@@ -493,7 +581,7 @@ __global__ __launch_bounds__(kWave * NW, GT > 0 ? 1 : kAdjLdsWpe) void bfgs_ba_a
           k1 = cr * sdv - rj * wdv; k2 = -rj * sdv;
           k3 = cr * swv - rj * wwv; k4 = -rj * swv;
         };
-        if constexpr (GVM) wide_pair_pass<GT, NW>(P, Pv, 0, k - 1, S, W, db, wb, gamma, hcoef, hd, hw, scratch, buf);
+        if constexpr (GVM) wide_pair_pass<GT, NW>(P, Pv, 0, k - 1, S, W, db, wb, gamma, hcoef, hd, hw, scratch, buf, nullptr, stage);
         else pair_pass<GM>(P, Pv, 0, k - 1, S, W, db, wb, gamma, hcoef, hd, hw, sp0, sp1, sp2, sp3, nullptr, lh, nlh);
       } else {
         each4([&](int i) {

@@ -545,7 +545,7 @@ __device__ __forceinline__ float wide_direction(int P, int Pv, int nh, const flo
           wg2 = pk_fma(w4[u].lo, gg[u].lo, wg2); wg2 = pk_fma(w4[u].hi, gg[u].hi, wg2);
         }
         float dd[4] = {sy2.x + sy2.y, wy2.x + wy2.y, sg2.x + sg2.y, wg2.x + wg2.y};
-        block_sum<4, NW>(dd, scratch, buf);
+        block_sum<4, NW, true>(dd, scratch, buf);
         buf ^= 1;
         const float rho = hrho[j], cr = hc[j] * rho;
         const float ay = fmaf(cr, dd[0], -(rho * dd[1])), by = -rho * dd[0];

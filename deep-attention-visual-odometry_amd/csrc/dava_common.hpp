@@ -106,10 +106,13 @@ __device__ __forceinline__ void wave_sums(float (&v)[R]) {
 // so ONE barrier per reduction suffices (NW = waves in the workgroup): a wave cannot reach the next use of
 // the same buffer before every wave has passed the intervening reduction's
 // barrier, i.e. before every wave finished reading this one.
-template <int R, int NW = kWaves>
+// SCALAR_WAVE: the wave index as a scalar (readfirstlane), so the partials' LDS address needs no
+// long-lived VGPR -- for the LDS-staged history passes, where a spilled address reload (a scratch load
+// and its vmcnt wait) would also wait for the staged copies in flight.
+template <int R, int NW = kWaves, bool SCALAR_WAVE = false>
 __device__ __forceinline__ void block_sum(float (&v)[R], float* scratch, int buf) {
   const int lane = threadIdx.x & (kWave - 1);
-  const int wave = threadIdx.x / kWave;
+  const int wave = SCALAR_WAVE ? __builtin_amdgcn_readfirstlane(threadIdx.x / kWave) : threadIdx.x / kWave;
   float* s = scratch + buf * (NW * 32);
   if constexpr (R >= 2) {
     float w[R];
