@@ -386,6 +386,24 @@ def test_global_vector_mode_equals_lds_mode(device, mode, xl, overrides):
     assert _rel(gv, lds).max() <= TOL
 
 
+@pytest.mark.parametrize("shape", [(4, 1500, False), (2, 2048, True)])
+def test_lds_staged_history_is_bitwise_the_register_pass(device, shape, overrides):
+    """The global-vector solve with the XL image streams its history rows HBM -> LDS by global_load_lds
+    one entry ahead (bfgs_solve.hip, wide_direction STAGED: rows of >= 3 float4 groups per thread, so
+    P > 4096 -- here 4521 and 6158); without the XL image (DAVA_GV_NO_XL) the same pass loads them into
+    registers.  The objective reads the same values from LDS or from the workspace, so the two solves --
+    parameters and status words -- must be bitwise equal."""
+    m, n, dist = shape
+    x0, obs, vis = _scene(4, m, n, dist, 963)
+    kw = dict(iterations=25, error_threshold=-1.0, minimum_step=-1.0, hessian_mode="compact")
+    overrides("FORCE_GV", 1)
+    staged, st_staged = _gpu_solve(device, x0, obs, vis, m, n, dist, **kw)
+    overrides("GV_NO_XL", 1)
+    regs, st_regs = _gpu_solve(device, x0, obs, vis, m, n, dist, **kw)
+    assert torch.isfinite(staged).all()
+    assert torch.equal(staged, regs) and torch.equal(st_staged, st_regs)
+
+
 @pytest.mark.parametrize("stopping", ["fixed", "reference"])
 def test_work_queue_launch_is_bitwise_invisible(device, stopping, overrides):
     """More problems than resident workgroups: with the work queue (a slot takes the next
