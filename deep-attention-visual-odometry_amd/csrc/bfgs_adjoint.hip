@@ -121,7 +121,7 @@ __device__ __forceinline__ void pair_pass(int P, int Pv, int j0, int j1, const f
                                           float* sp2, float* sp3, const float* R1_j0 = nullptr,
                                           const float* LR = nullptr, int nl = 0) {
   const int lane = threadIdx.x & (kWave - 1);
-  const int wave = threadIdx.x / kWave;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);  // scalar: row addresses wave-uniform
   const int G = (P + 3) / 4;
   f4a pa[GM], pb[GM];
   bool ok[GM];

@@ -271,7 +271,7 @@ __device__ __forceinline__ void compact_products(int P, int Pv, int nh, const fl
                                  float* coef, const float* hrho, const float* hc, float gamma0, const float* g,
                                  const float* gp, float* a_out, float* b_out) {
   const int lane = threadIdx.x & (kWave - 1);
-  const int wave = threadIdx.x / kWave;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);  // scalar: row addresses wave-uniform
   const int G = (P + 3) / 4;
   for (int j = wave; j < nh; j += NW) {
     const float* sr = S + (size_t)j * Pv;
@@ -706,7 +706,10 @@ __device__ __forceinline__ void compact_products_fused(int P, int Pv, int nh, co
   static_assert(NW == 1 || NW == 2 || NW == 4, "the cross-wave combine is written for 1, 2 or 4 waves");
   constexpr int EF = fused_inflight<GM>();
   const int lane = threadIdx.x & (kWave - 1);
-  const int wave = threadIdx.x / kWave;
+  // the wave index as a scalar: the entry index j (and so each row's buffer descriptor) is then
+  // provably wave-uniform; from threadIdx.x / 64 the compiler cannot tell, keeps the descriptor in
+  // VGPRs and wraps every buffer load in a waterfall loop (readfirstlane x 4, compares, exec juggling)
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
   const int G = (P + 3) / 4;
   f4v pa[GM], pb[GM];
   bool ok[GM];

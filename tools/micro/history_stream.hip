@@ -4,6 +4,7 @@
 // of GM float4 groups per lane; per entry the four dots, one transposed wave reduction and the two
 // accumulations the solve does.  Layouts: 0 = per problem an S block then a W block (the solve's),
 // 1 = S_j and W_j adjacent.  Prints GB/s of history rows read.
+// usage: history_stream [P] [1: non-zero rows] [x: solve layout only]
 // build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -I../../deep-attention-visual-odometry_amd/csrc
 //        -I../../include history_stream.hip -o history_stream
 #include <hip/hip_runtime.h>
@@ -86,6 +87,11 @@ __global__ __launch_bounds__(64 * NW) void stream_kernel(const float* __restrict
   if (t == 12345.f) out[blockIdx.x * 64 * NW + threadIdx.x] = t;  // keep the work
 }
 
+__global__ void fill_rows(float* p, size_t n) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    p[i] = 1e-3f * (float)((i * 2654435761u) % 1000u) - 0.5f;
+}
+
 template <int GM, int EF, int NW, int LAYOUT>
 void run(const char* tag, const float* hist, int B, int P, int Pv, int kcap, int iters, float* out) {
   hipEvent_t a, b;
@@ -112,9 +118,14 @@ int main(int argc, char** argv) {
   float *hist, *out;
   hipMalloc(&hist, (size_t)Bmax * 2 * kcap * Pv * 4);
   hipMemset(hist, 0, (size_t)Bmax * 2 * kcap * Pv * 4);
+  if (argc > 2 && atoi(argv[2]) == 1) {  // non-zero rows (the solve's rows are never all zero)
+    const size_t n = (size_t)Bmax * 2 * kcap * Pv;
+    hipLaunchKernelGGL(fill_rows, dim3(4096), dim3(256), 0, 0, hist, n);
+  }
   hipMalloc(&out, (size_t)Bmax * 1024 * 4);
   for (int B : {64, 256, 512, 1024, 2048}) {
     run<2, 4, 2, 0>("c2 pass (solve layout)", hist, B, P, Pv, kcap, iters, out);
+    if (argc > 3) continue;  // the solve layout only
     run<2, 4, 2, 1>("c2 pass (S_j W_j adjacent)", hist, B, P, Pv, kcap, iters, out);
     run<2, 8, 2, 0>("c2 pass EF 8", hist, B, P, Pv, kcap, iters, out);
     run<2, 4, 1, 0>("c2 pass one wave", hist, B, P, Pv, kcap, iters, out);
