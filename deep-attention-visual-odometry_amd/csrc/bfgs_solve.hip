@@ -646,6 +646,10 @@ __device__ __forceinline__ float wide_direction(int P, int Pv, int nh, const flo
           const float di = -1.0f * (pb[u][e] + sri * (c * sg) - sri * hyg - pa[u][e] * rsg);
           d[i] = di;
           dg += di * gu[e];
+        } else if constexpr (staged) {
+          // the staged copies filled whole groups of d's slot with the last entry's W-row pads: the
+          // pads [P, Pv) of d are zero again before the objective reads x + alpha d in float4 groups
+          d[i] = 0.f;
         }
       }
       *reinterpret_cast<f4v*>(s_row + 4 * q) = sv[u];  // history entry `entry` = (s, H'y, rho, c)

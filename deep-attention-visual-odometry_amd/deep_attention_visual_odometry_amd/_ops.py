@@ -296,9 +296,20 @@ def _(x_out_grad, tape, status, observations, visibility, num_views, num_points,
 # ------------------------------------------------- generic BFGS building blocks
 
 def _square_batch(h: Tensor) -> Tuple[int, int]:
-    if h.dim() != 3 or h.shape[1] != h.shape[2]:
-        raise ValueError(f"expected a (B, n, n) batch of matrices, got {tuple(h.shape)}")
+    # the kernels (GPU and host) read raw row-major pointers: a transposed or sliced view would be
+    # computed on the wrong layout, and empty_like would copy its strides into the outputs
+    if h.dim() != 3 or h.shape[1] != h.shape[2] or not h.is_contiguous():
+        raise ValueError(f"expected a contiguous (B, n, n) batch of matrices, got {tuple(h.shape)} "
+                         f"(contiguous={h.is_contiguous()})")
     return h.shape[0], h.shape[1]
+
+
+def _row_batch(t: Tensor, what: str) -> Tuple[int, int]:
+    """The primary (B, n) operand of an op: contiguous, for the same reason as _square_batch."""
+    if t.dim() != 2 or not t.is_contiguous():
+        raise ValueError(f"{what}: expected a contiguous (B, n) batch, got {tuple(t.shape)} "
+                         f"(contiguous={t.is_contiguous()})")
+    return t.shape[0], t.shape[1]
 
 
 def _same(t: Tensor, like: Tensor, shape, what: str) -> None:
@@ -350,7 +361,7 @@ def _(h, s, y, grad, need_h, need_s, need_y):
 @torch.library.custom_op("dava::bfgs_initial_scale", mutates_args=(), device_types=_CUDA)
 def bfgs_initial_scale(s: Tensor, y: Tensor) -> Tensor:
     """(B, n), (B, n) -> gamma (B,) (``bfgs_solver.py:217-233``)."""
-    b, n = s.shape
+    b, n = _row_batch(s, "step")
     _same(y, s, (b, n), "delta_gradient")
     out = s.new_empty((b,))
     with torch.cuda.device(s.device):
@@ -367,7 +378,7 @@ def _(s, y):
 @torch.library.custom_op("dava::bfgs_initial_scale_backward", mutates_args=(), device_types=_CUDA)
 def bfgs_initial_scale_backward(s: Tensor, y: Tensor, grad: Tensor, need_s: bool,
                                 need_y: bool) -> Tuple[Tensor, Tensor]:
-    b, n = s.shape
+    b, n = _row_batch(s, "step")
     _same(grad, s, (b,), "grad")
     gs = torch.empty_like(s) if need_s else _empty0(s)
     gy = torch.empty_like(y) if need_y else _empty0(s)
@@ -465,7 +476,7 @@ WOLFE_FLAG_COLUMNS = 2
 @torch.library.custom_op("dava::wolfe_init", mutates_args=(), device_types=_CUDA)
 def wolfe_init(direction: Tensor, f0: Tensor, g0: Tensor) -> Tuple[Tensor, Tensor]:
     """(state (B, 9), flags (B, 2) uint8) for a line search along ``direction`` from (f0, g0)."""
-    b, n = direction.shape
+    b, n = _row_batch(direction, "search_direction")
     _same(g0, direction, (b, n), "base_gradient")
     _same(f0, direction, (b,), "base_error")
     state = direction.new_empty((b, WOLFE_STATE_COLUMNS))
@@ -559,7 +570,7 @@ def _(h, s, y, grad, need_h, need_s, need_y):
 
 @bfgs_initial_scale.register_kernel("cpu")
 def _(s, y):
-    b, n = s.shape
+    b, n = _row_batch(s, "step")
     _same(y, s, (b, n), "delta_gradient")
     out = s.new_empty((b,))
     _cpu("bfgs_initial_scale", s, b, n, N.ptr(s), N.ptr(y), N.ptr(out))
@@ -568,7 +579,7 @@ def _(s, y):
 
 @bfgs_initial_scale_backward.register_kernel("cpu")
 def _(s, y, grad, need_s, need_y):
-    b, n = s.shape
+    b, n = _row_batch(s, "step")
     _same(grad, s, (b,), "grad")
     gs = torch.empty_like(s) if need_s else _empty0(s)
     gy = torch.empty_like(y) if need_y else _empty0(s)
@@ -619,7 +630,7 @@ def _(h, g, grad, need_h, need_g):
 
 @wolfe_init.register_kernel("cpu")
 def _(direction, f0, g0):
-    b, n = direction.shape
+    b, n = _row_batch(direction, "search_direction")
     _same(g0, direction, (b, n), "base_gradient")
     _same(f0, direction, (b,), "base_error")
     state = direction.new_empty((b, WOLFE_STATE_COLUMNS))

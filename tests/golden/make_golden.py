@@ -734,9 +734,38 @@ def gen_distortion_masked():
     np.savez_compressed(os.path.join(HERE, "distortion_masked.npz"), **out)
 
 
+def gen_c5():
+    """BFGSSolver(iterations=K, error_threshold=-1, minimum_step=-1).eval() of the REAL reference at the
+    C5 shape (16 views x 4096 points, pinhole, P = 12,381) on the bench's own first two C5 problems
+    (bench.py defaults: seed 20251015 + 3000, first index 0, every pair visible), K = 20 and 100, fp32.
+
+    The ±1-ulp-nudged starts (x0 moved to the next float up / down in every component) are solved too,
+    so the per-block envelopes (the reference's own sensitivity) ship in the fixture: at this shape the
+    dense reference holds a 613 MB inverse Hessian per problem, and a GPU test cannot afford to rerun it.
+    Run time here: about 10 s per iteration per run (8 threads), ~1 h for the six runs."""
+    import time
+
+    m, n = 16, 4096
+    s = make_scenes(2, m, n, distortion=False, seed=20251015 + 3000)
+    x0, obs, vis = torch.tensor(s.initial), torch.tensor(s.observations), torch.tensor(s.visibility)
+    out = {"x0": x0.numpy(), "obs": obs.numpy(), "vis": vis.numpy()}
+    fn = closure_for(obs, vis, m, n)
+    starts = {"": x0, "_up": torch.nextafter(x0, torch.full_like(x0, float("inf"))),
+              "_down": torch.nextafter(x0, torch.full_like(x0, -float("inf")))}
+    for k in (20, 100):
+        for tag, start in starts.items():
+            t = time.time()
+            res = BFGSSolver(iterations=k, error_threshold=-1.0, minimum_step=-1.0).eval()(start, fn)
+            out[f"k{k}{tag}"] = res.numpy()
+            print(f"c5 K={k}{tag}: {time.time() - t:.0f} s", flush=True)
+            np.savez_compressed(os.path.join(HERE, "c5_traj.npz"), **out)
+
+
 if __name__ == "__main__":
     torch.set_num_threads(8)
     which = sys.argv[1:] or ["eval", "update", "ls", "traj", "ray", "grad", "train", "l1", "l1grad", "bc", "bcmask"]
+    if "c5" in which:  # not in the default set: ~1 h of CPU
+        gen_c5()
     if "bc" in which:
         gen_distortion()
     if "bcmask" in which:

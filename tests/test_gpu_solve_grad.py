@@ -517,6 +517,34 @@ def test_gv_adjoint_forms_agree(device, waves, gd_hbm, overrides):
         assert rx.max() <= 1e-4 and ro.max() <= 1e-4, (rx, ro)
 
 
+@pytest.mark.parametrize("waves,m,n,k,b", [
+    ("8", 4, 2800, 8, 2),    # P = 8421: 2106 groups over 512 threads -> GT = 7 (one entry per reduction, staged)
+    ("4", 16, 4096, 4, 1),   # P = 12381 (C5): 3096 groups over 256 threads -> GT = 14, the four-wave staged form
+])
+def test_gv_adjoint_staged_rows_are_bitwise_the_register_pass(device, waves, m, n, k, b, overrides):
+    """The GV adjoint's row passes stage each entry's rows through the HVP's dual gradient slots in LDS
+    (global_load_lds one entry ahead, csrc/bfgs_adjoint.hip) whenever the dual gradient lives in LDS and one
+    entry is consumed per reduction (GT x waves > 32, i.e. P > 8192 at eight waves).  With the dual gradient in
+    the workspace (DAVA_ADJ_GD_HBM) the same passes read the rows into registers: same rows, dots and sums in
+    the same order, so the gradients must be bitwise equal.  A wrong ownership, offset or wait in the staged
+    copy shows up here, which the oracle comparison at 2e-3 could miss."""
+    from deep_attention_visual_odometry_amd import make_scenes
+
+    overrides("ADJ_GV_WAVES", int(waves))
+    s = make_scenes(b, m, n, distortion=False, seed=939 + n, drop=0.1)
+    x0, obs, vis = (torch.tensor(t).to(device) for t in (s.initial, s.observations, s.visibility))
+    vis = vis.to(torch.uint8)
+    w = torch.randn(x0.shape, generator=torch.Generator().manual_seed(8)).to(device)
+    x, status, tape = torch.ops.dava.ba_solve_record(x0, obs, vis, m, n, False, 1e-4, 0.9, -1.0, k, -1.0, 1000,
+                                                     True, 0)
+    assert (status[:, 0] == k).all() and torch.isfinite(x).all()
+    gx, gobs = torch.ops.dava.ba_solve_backward(w, tape, status, obs, vis, m, n, False, k, 0, True)
+    overrides("ADJ_GD_HBM", 1)
+    gx2, gobs2 = torch.ops.dava.ba_solve_backward(w, tape, status, obs, vis, m, n, False, k, 0, True)
+    assert torch.isfinite(gx).all() and gx.abs().max() > 0
+    assert torch.equal(gx2, gx) and torch.equal(gobs2, gobs)
+
+
 def test_gv_recording_is_bitwise_the_gv_solve(device, overrides):
     """A global-vector-mode recording (DAVA_FORCE_GV at the C3 shape: the forward's vectors in the
     tape's own region, wide history pass writing the tape rows) returns exactly the GV solve's x and

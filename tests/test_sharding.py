@@ -122,6 +122,12 @@ def test_bench_launches_its_own_ranks():
     assert line["config"]["global_batch"] == 10
     assert line["config"]["gathered_rows"] == 10
     assert line["config"]["gathered_matches_inputs"] is True
+    # the N > 1 line splits each rank's step into its own solve and the all-gather, and rank 0 spot-checks
+    # rows of the gathered batch (against the identity stub's inputs here, the oracle on the GPU)
+    ranks = line["per_rank"]
+    assert len(ranks["solve_ms"]) == 2 and len(ranks["all_gather_ms"]) == 2
+    assert all(t >= 0 for t in ranks["solve_ms"] + ranks["all_gather_ms"])
+    assert line["spot_check"]["identity_stub_rows_equal_inputs"] is True
 
 
 def test_packed_gather_round_trips_status_bits():

@@ -7,7 +7,10 @@
 #   configs               tools/measure_configs.sh (one bench line per configuration)
 #   profile=TAG           tools/profile.sh TAG (kernel trace + FETCH_SIZE + WRITE_SIZE passes, C3)
 #   profile_c5=TAG        tools/profile.sh TAG on the C5 configuration
+#   profile_cfg=TAG:ARGS  tools/profile.sh TAG with bench ARGS (e.g. the C2 configuration)
 #   sq=TAG[:BENCH_ARGS]   tools/pmc_sq.sh (SQ busy/VALU/MFMA counters) for a configuration
+#   micro=P               tools/micro/solve_pass_stream P (the history pass alone; P > 512: the headline's rows)
+#   eval=TAG              tools/eval_sweep.py (C3, C5) + tools/profile_eval.sh TAG for both
 #   ab=SPEC;SPEC...       tools/ab_env.sh with the given specs (BENCH_ARGS from the environment)
 # usage: tools/gpu_run.sh tests smoke bench profile=r02a
 set -uo pipefail
@@ -48,6 +51,24 @@ for s in "$@"; do
       tools/profile.sh "$val" --batch 256 --views 16 --points 4096 --no-distortion --steps 2 --warmup 1 \
         > gpurun_out/prof_$val.log 2>&1 || { tail -5 gpurun_out/prof_$val.log; exit 1; }
       tail -1 gpurun_out/prof_$val.log ;;
+    profile_cfg)
+      step profile_cfg "$val"
+      tag=${val%%:*}; args=${val#*:}
+      tools/profile.sh "$tag" $args > gpurun_out/prof_$tag.log 2>&1 || { tail -5 gpurun_out/prof_$tag.log; exit 1; }
+      tail -1 gpurun_out/prof_$tag.log ;;
+    micro)
+      step micro "$val"
+      timeout -k 10 300 tools/micro/solve_pass_stream "$val" > gpurun_out/micro_$val.log 2>&1 \
+        || { tail -5 gpurun_out/micro_$val.log; exit 1; }
+      cat gpurun_out/micro_$val.log ;;
+    eval)
+      step eval "$val"
+      timeout -k 10 300 python3 tools/eval_sweep.py > gpurun_out/eval_sweep_$val.jsonl 2>gpurun_out/eval_sweep_$val.err \
+        || { tail -5 gpurun_out/eval_sweep_$val.err; exit 1; }
+      cut -c1-400 gpurun_out/eval_sweep_$val.jsonl
+      for c in C3 C5; do
+        tools/profile_eval.sh "$val" $c > gpurun_out/prof_eval_${val}_$c.log 2>&1 || { tail -5 gpurun_out/prof_eval_${val}_$c.log; exit 1; }
+      done ;;
     sq)
       step sq "$val"
       tag=${val%%:*}; args=${val#*:}; [ "$args" = "$val" ] && args=""

@@ -2,7 +2,10 @@
 # SQ instruction-mix / stall / VALU / MFMA counters of the solve kernel (one rocprofv3 pass per set,
 # kernel trace only -- no sys/runtime traces with --pmc, as the pool requires).
 # usage: tools/pmc_sq.sh TAG [bench args...]    -> gpurun_out/sq_TAG/p{1,2,3}/..., summary on stdout
+#        KERNEL=ba_evaluate_kernel PROG=tools/eval_sweep.py tools/pmc_sq.sh TAG [prog args...]
+#        (another program and kernel: PROG runs with the given args instead of bench.py's)
 set -uo pipefail
+KERNEL=${KERNEL:-bfgs_ba_solve_kernel}
 TAG=$1; shift
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/sq_$TAG
@@ -14,17 +17,26 @@ C="SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F32 SQ_THREAD_
 i=0
 for set in "$A" "$B" "$C"; do
   i=$((i+1))
-  timeout -s KILL 120 rocprofv3 --pmc $set -d "$OUT/p$i" -o p$i --output-format csv -- \
-    python3 "$R/bench.py" --cpu-sample 0 --steps 1 --warmup 0 "$@" > "$OUT/p$i.log" 2>&1 || { echo "pass $i failed"; tail -5 "$OUT/p$i.log"; exit 1; }
+  if [ -n "${PROG:-}" ]; then
+    timeout -s KILL 120 rocprofv3 --pmc $set -d "$OUT/p$i" -o p$i --output-format csv -- \
+      python3 "$R/$PROG" "$@" > "$OUT/p$i.log" 2>&1 || { echo "pass $i failed"; tail -5 "$OUT/p$i.log"; exit 1; }
+  else
+    timeout -s KILL 120 rocprofv3 --pmc $set -d "$OUT/p$i" -o p$i --output-format csv -- \
+      python3 "$R/bench.py" --cpu-sample 0 --steps 1 --warmup 0 "$@" > "$OUT/p$i.log" 2>&1 || { echo "pass $i failed"; tail -5 "$OUT/p$i.log"; exit 1; }
+  fi
 done
-python3 - "$OUT" <<'PY'
+python3 - "$OUT" "$KERNEL" <<'PY'
 import csv, glob, sys, collections
-out = sys.argv[1]
+out, kernel = sys.argv[1], sys.argv[2]
 tot = collections.defaultdict(float)
+launches = collections.defaultdict(set)
 for f in glob.glob(out + "/p*/**/*counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):
-        if "bfgs_ba_solve_kernel" in r["Kernel_Name"]:
+        if kernel in r["Kernel_Name"]:
             tot[r["Counter_Name"]] += float(r["Counter_Value"])
+            launches[f].add(r.get("Dispatch_Id", r.get("Correlation_Id", "")))
+n = max((len(v) for v in launches.values()), default=1)
+print(f"kernel {kernel}: counters summed over {n} launch(es) per pass (divide by it for per-launch figures)")
 for k, v in sorted(tot.items()):
     print(f"{k:28s} {v:.4g}")
 CUS, SIMDS, XCDS = 256, 1024, 8
