@@ -79,6 +79,9 @@ def parse(argv=None):
     p.add_argument("--differentiate", action="store_true",
                    help="time the solve AND its gradient (recording solve + adjoint kernel, d(w.x)/d(x0, obs)) -- "
                         "the reference's create_graph mode; not the headline metric")
+    p.add_argument("--no-live-counters", action="store_true",
+                   help="skip the rocprofv3 FETCH_SIZE / WRITE_SIZE child passes and the history-stream ceiling run "
+                        "that follow the timed region at N = 1 (roofline.traffic then comes from the committed summary)")
     p.add_argument("--launch-test", action="store_true",
                    help="multi-rank LAUNCH plumbing check on CPU (gloo, identity stub instead of the solve); "
                         "prints a line marked as a launch test, never a measurement")
@@ -442,6 +445,76 @@ def main():
         dist.destroy_process_group()
 
 
+def _config_argv(args):
+    """This configuration's flags, for a child bench process that must run the same workload."""
+    out = ["--batch", str(args.batch), "--views", str(args.views), "--points", str(args.points),
+           "--iterations", str(args.iterations), "--mode", args.mode, "--residual", args.residual,
+           "--seed", str(args.seed), "--error-threshold", str(args.error_threshold),
+           "--minimum-step", str(args.minimum_step)]
+    return out + (["--no-distortion"] if args.no_distortion else [])
+
+
+def live_traffic(args, kernel="bfgs_ba_solve_kernel"):
+    """HBM (fabric) bytes per launch of the solve kernel, measured in THIS run: two rocprofv3 --pmc passes
+    (FETCH_SIZE, then WRITE_SIZE: they cannot share a pass) over a child bench process that runs one launch of
+    the same configuration, started after the timed region (a child process; nothing here is exec'd).
+    Corrected as MI355X_MICROARCH.md's HBM section prescribes: read = 2 x FETCH_SIZE (gfx950 tallies a
+    16 B/lane streaming read at half its bytes), write = WRITE_SIZE, KiB -> bytes.  None (with the reason)
+    if rocprofv3 is unavailable or a pass fails."""
+    import csv
+    import shutil
+    import tempfile
+
+    prof = shutil.which("rocprofv3") or ("/opt/rocm/bin/rocprofv3" if os.path.exists("/opt/rocm/bin/rocprofv3") else None)
+    if prof is None:
+        return None, "rocprofv3 not found"
+    vals = {}
+    with tempfile.TemporaryDirectory(prefix="dava_pmc_", dir="/tmp") as tmp:
+        for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+            out = os.path.join(tmp, counter)
+            cmd = [prof, "--pmc", counter, "-d", out, "-o", "p", "--output-format", "csv", "--",
+                   sys.executable, os.path.abspath(__file__), "--steps", "1", "--warmup", "0", "--cpu-sample", "0",
+                   "--no-live-counters"] + _config_argv(args)
+            env = dict(os.environ, TMPDIR="/tmp")
+            try:
+                r = subprocess.run(cmd, cwd="/tmp", env=env, capture_output=True, text=True, timeout=180)
+            except subprocess.TimeoutExpired:
+                return None, f"{counter} pass timed out"
+            if r.returncode != 0:
+                return None, f"{counter} pass exited {r.returncode}: {r.stderr[-300:]}"
+            rows = []
+            for root, _, files in os.walk(out):
+                for f in files:
+                    if f.endswith("counter_collection.csv"):
+                        with open(os.path.join(root, f)) as fh:
+                            rows += [row for row in csv.DictReader(fh)
+                                     if kernel in row["Kernel_Name"] and row["Counter_Name"] == counter]
+            if not rows:
+                return None, f"{counter}: no {kernel} rows in the counter output"
+            vals[counter] = sum(float(row["Counter_Value"]) for row in rows) / len(rows)
+    return 2.0 * 1024.0 * vals["FETCH_SIZE"] + 1024.0 * vals["WRITE_SIZE"], vals
+
+
+def live_ceiling(p):
+    """The headline's history stream alone (tools/micro/solve_pass_stream P ceiling: the solve's own LDS-mode
+    history pass over C3's rows, B = 8192, 6 LDS-resident entries, every resident problem streaming all the
+    time), run as a child process after the timed region: the rate this access pattern reaches with no
+    objective evaluation beside it.  Returns (ms, GB/s of history rows) or None."""
+    exe = os.path.join(REPO, "tools", "micro", "solve_pass_stream")
+    if not os.path.exists(exe):
+        return None
+    try:
+        r = subprocess.run([exe, str(p), "ceiling"], capture_output=True, text=True, timeout=120)
+    except subprocess.TimeoutExpired:
+        return None
+    for line in r.stdout.splitlines():
+        if "B= 8192" in line and "ms" in line:
+            ms = float(line.split(":")[-1].split("ms")[0])
+            gbs = float(line.split("ms")[1].split("GB/s")[0])
+            return ms, gbs
+    return None
+
+
 GOLDEN_C5 = os.path.join(REPO, "tests", "golden", "c5_traj.npz")
 
 
@@ -619,6 +692,27 @@ def measurement_line(args, line, world, b, p, mn, distortion, ray, plan, kernel_
                    else (None, None))
     if parity is None and fixed_k:
         parity = golden_parity(args, x0_cpu, x)
+    if roofline is not None and world == 1 and not args.no_live_counters:
+        measured, detail = live_traffic(args)
+        if measured is not None:
+            roofline["traffic"] = measured
+            roofline["traffic_source"] = ("measured in this run: rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE "
+                                          "passes (child processes, one launch of this configuration each, after "
+                                          "the timed region); read = 2 x FETCH_SIZE, write = WRITE_SIZE "
+                                          f"(KiB: {detail})")
+            roofline["traffic_over_algorithmic"] = round(measured / algo, 4)
+        else:
+            roofline["traffic_live_failed"] = detail
+        if headline:
+            ceil = live_ceiling(p)
+            if ceil is not None:
+                roofline["measured_ceiling"] = {
+                    "ms": ceil[0], "GBps_history_reads": ceil[1],
+                    "frac_of_measured_ceiling": round(ceil[0] / launch_ms, 4),
+                    "source": "tools/micro/solve_pass_stream 794 ceiling, run in this session after the timed "
+                              "region: the solve's own history pass over the same rows (B = 8192, 6 LDS-resident "
+                              "entries, 512 problems resident), nothing else on the CU; frac = its time / the "
+                              "solve's launch time"}
     line.update({
         "metric": f"BA problems/sec (B={b} per GPU, {args.views} views x {args.points} pts"
                   f"{', Brown-Conrady' if distortion else ''}{', ray-angle residual' if ray else ''}, "

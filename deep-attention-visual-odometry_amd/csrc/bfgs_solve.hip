@@ -1327,13 +1327,24 @@ struct EvalArgs {
   float* slope;
 };
 
-template <bool GRAD, bool SLOPE, bool TRIAL, bool GV, int RES>
-__global__ __launch_bounds__(kBlock) void ba_evaluate_kernel(EvalArgs a) {
+// The evaluation the solve runs per line-search trial, as one launch (dava_ba_evaluate), with the solve's
+// own layout per mode so that it measures -- and, as the generic path's closure, runs -- the same sweep:
+//   LDS mode (P fits on-chip): x, d, gradient, observations and visibility staged in LDS, NW = 4 waves,
+//     PPT = 1 when every point has a thread (C1-C3: each thread's point in registers across the views);
+//   GV + XL (C5: 8 waves, one problem per CU): x, d and the gradient in LDS (3 Pv floats), observations
+//     and visibility read in place, the packed pair sweep (two points per step) -- the in-solve trial;
+//   GV without XL (an image past the LDS): x, d and the gradient in place in HBM.
+// (Before r05 the GV form ran 4 waves with the vectors in HBM: at C5 VALUBusy 40% and 4.2x the
+// algorithmic bytes from the per-view read-modify-write of the point gradients, profiles/r05_eval_*.)
+template <bool GRAD, bool SLOPE, bool TRIAL, bool GV, int RES, bool XL = false, int NW = kWaves, int PPT = 0>
+__global__ __launch_bounds__(kWave * NW) void ba_evaluate_kernel(EvalArgs a) {
+  static_assert(!XL || GV, "XL is a global-vector-mode variant");
+  constexpr int BLOCK = kWave * NW;
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const Layout L = a.L;
   const int P = L.P, M = L.M, N = L.N, Pv = a.Pv;
   const int b = blockIdx.x, tid = threadIdx.x;
-  const LdsCarve cv = carve_lds(M, N, Pv, 0, GV);
+  const LdsCarve cv = carve_lds(M, N, Pv, 0, GV, 0, XL, NW);
   const int MN = M * N;
   float* views = lds + cv.views;
   float* vpart = lds + cv.vpart;
@@ -1343,7 +1354,7 @@ __global__ __launch_bounds__(kBlock) void ba_evaluate_kernel(EvalArgs a) {
   float* g;
   const float* obs;
   const uint8_t* vis;
-  if (GV) {  // large P: work on the caller's buffers in place
+  if (GV && !XL) {  // an image past the LDS: work on the caller's buffers in place
     x = a.x + (size_t)b * P;
     d = a.dir ? a.dir + (size_t)b * P : nullptr;
     g = a.grad ? a.grad + (size_t)b * P : nullptr;
@@ -1352,29 +1363,36 @@ __global__ __launch_bounds__(kBlock) void ba_evaluate_kernel(EvalArgs a) {
   } else {
     float* xl = lds + cv.x;
     float* dl = lds + cv.d;
-    float* gl = lds + cv.g0;
-    float* ol = lds + cv.obs;
-    uint8_t* vl = reinterpret_cast<uint8_t*>(lds) + cv.vis_bytes_off;
-    for (int i = tid; i < Pv; i += kBlock) {
+    float* gl = lds + (XL ? cv.ge : cv.g0);
+    for (int i = tid; i < Pv; i += BLOCK) {
       xl[i] = i < P ? a.x[(size_t)b * P + i] : 0.f;
       dl[i] = (a.dir && i < P) ? a.dir[(size_t)b * P + i] : 0.f;
       gl[i] = 0.f;
     }
-    for (int i = tid; i < 2 * MN; i += kBlock) ol[i] = a.obs[(size_t)b * 2 * MN + i];
-    for (int i = tid; i < MN; i += kBlock) vl[i] = a.vis[(size_t)b * MN + i] ? 1 : 0;
-    x = xl; d = dl; g = gl; obs = ol; vis = vl;
+    if constexpr (GV) {  // XL: the scene stays in HBM, read in place as the solve does
+      obs = a.obs + (size_t)b * 2 * MN;
+      vis = a.vis + (size_t)b * MN;
+    } else {
+      float* ol = lds + cv.obs;
+      uint8_t* vl = reinterpret_cast<uint8_t*>(lds) + cv.vis_bytes_off;
+      for (int i = tid; i < 2 * MN; i += BLOCK) ol[i] = a.obs[(size_t)b * 2 * MN + i];
+      for (int i = tid; i < MN; i += BLOCK) vl[i] = a.vis[(size_t)b * MN + i] ? 1 : 0;
+      obs = ol; vis = vl;
+    }
+    x = xl; d = dl; g = gl;
   }
   __syncthreads();
   const float al = (TRIAL && a.alpha) ? a.alpha[b] : 0.f;
   int buf = 0;
   float E = 0.f, sl = 0.f;
-  ba_eval<GRAD, SLOPE, TRIAL, false, false, RES, float>(L, x, d, al, obs, vis, g, views, vpart, scratch, buf, E, sl);
+  ba_eval<GRAD, SLOPE, TRIAL, false, false, RES, float, NW, PPT, GV>(L, x, d, al, obs, vis, g, views, vpart, scratch,
+                                                                     buf, E, sl);
   if (tid == 0) {
     a.err[b] = E;
     if (SLOPE && a.slope) a.slope[b] = sl;
   }
-  if (GRAD && a.grad && !GV)
-    for (int i = tid; i < P; i += kBlock) a.grad[(size_t)b * P + i] = g[i];
+  if (GRAD && a.grad && (!GV || XL))
+    for (int i = tid; i < P; i += BLOCK) a.grad[(size_t)b * P + i] = g[i];
 }
 
 static int check_scene(const DavaScene* s, bool need_data = true) {
@@ -1755,24 +1773,29 @@ extern "C" int dava_ba_solve_record(const DavaScene* scene, const DavaSolverConf
   return solve_impl(scene, config, x0, x_out, error_out, status_out, tape, tape_bytes, true, stream);
 }
 
-template <bool G, bool S, bool T, bool GV, int RES>
-static void launch_eval_gv(const EvalArgs& a, int B, int lds, hipStream_t s) {
+template <bool G, bool S, bool T, bool GV, int RES, bool XL, int NW, int PPT>
+static void launch_eval_form(const EvalArgs& a, int B, int lds, hipStream_t s) {
+  const auto kernel = ba_evaluate_kernel<G, S, T, GV, RES, XL, NW, PPT>;
   if (lds > 64 * 1024)
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(ba_evaluate_kernel<G, S, T, GV, RES>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-  hipLaunchKernelGGL((ba_evaluate_kernel<G, S, T, GV, RES>), dim3(B), dim3(kBlock), lds, s, a);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+  hipLaunchKernelGGL(kernel, dim3(B), dim3(kWave * NW), lds, s, a);
+}
+
+// form: 0 = LDS mode, PPT 0 | 1 = LDS mode, a point per thread in registers | 2 = GV + XL (8 waves) |
+// 3 = GV in place (8 waves)
+template <bool G, bool S, bool T, int RES>
+static void launch_eval_res(const EvalArgs& a, int B, int lds, hipStream_t s, int form) {
+  constexpr int GVW = solve_waves(true);
+  if (form == 3) launch_eval_form<G, S, T, true, RES, false, GVW, 0>(a, B, lds, s);
+  else if (form == 2) launch_eval_form<G, S, T, true, RES, true, GVW, 0>(a, B, lds, s);
+  else if (form == 1) launch_eval_form<G, S, T, false, RES, false, kWaves, 1>(a, B, lds, s);
+  else launch_eval_form<G, S, T, false, RES, false, kWaves, 0>(a, B, lds, s);
 }
 
 template <bool G, bool S, bool T>
-static void launch_eval(const EvalArgs& a, int B, int lds, hipStream_t s, bool gv, int res) {
-  constexpr int SQ = DAVA_RESIDUAL_SQUARED_REPROJECTION, RAY = DAVA_RESIDUAL_RAY_ANGLE;
-  if (res == RAY) {
-    if (gv) launch_eval_gv<G, S, T, true, RAY>(a, B, lds, s);
-    else launch_eval_gv<G, S, T, false, RAY>(a, B, lds, s);
-  } else {
-    if (gv) launch_eval_gv<G, S, T, true, SQ>(a, B, lds, s);
-    else launch_eval_gv<G, S, T, false, SQ>(a, B, lds, s);
-  }
+static void launch_eval(const EvalArgs& a, int B, int lds, hipStream_t s, int form, int res) {
+  if (res == DAVA_RESIDUAL_RAY_ANGLE) launch_eval_res<G, S, T, DAVA_RESIDUAL_RAY_ANGLE>(a, B, lds, s, form);
+  else launch_eval_res<G, S, T, DAVA_RESIDUAL_SQUARED_REPROJECTION>(a, B, lds, s, form);
 }
 
 extern "C" int dava_ba_evaluate(const DavaScene* scene, const float* x, const float* direction, const float* alpha,
@@ -1783,7 +1806,10 @@ extern "C" int dava_ba_evaluate(const DavaScene* scene, const float* x, const fl
   if (!x || !error_out) return DAVA_ERR_INVALID_ARGUMENT;
   if (slope_out && !direction) return DAVA_ERR_INVALID_ARGUMENT;
   const bool gv = use_gv(scene);
-  const int lds = lds_bytes_for(scene, 0, gv);
+  const int gvw = solve_waves(true);
+  const bool xl = gv && !debug_flag(kDbgGVNoXL) && lds_bytes_for(scene, 0, true, 0, true, gvw) <= kMaxLds;
+  const int form = gv ? (xl ? 2 : 3) : (scene->num_points <= kBlock && !debug_flag(kDbgNoPPT) ? 1 : 0);
+  const int lds = gv ? lds_bytes_for(scene, 0, true, 0, xl, gvw) : lds_bytes_for(scene, 0, false);
   if (lds > kMaxLds) return DAVA_ERR_UNSUPPORTED;
   EvalArgs a;
   a.L = Layout{scene->num_views, scene->num_points, scene->num_parameters, scene->distortion ? 1 : 0};
@@ -1799,13 +1825,13 @@ extern "C" int dava_ba_evaluate(const DavaScene* scene, const float* x, const fl
   hipStream_t s = static_cast<hipStream_t>(stream);
   const bool G = grad_out != nullptr, S = slope_out != nullptr, T = direction != nullptr && alpha != nullptr;
   const int B = scene->batch;
-  if (G && S && T) launch_eval<true, true, true>(a, B, lds, s, gv, scene->residual);
-  else if (G && S) launch_eval<true, true, false>(a, B, lds, s, gv, scene->residual);
-  else if (G && T) launch_eval<true, false, true>(a, B, lds, s, gv, scene->residual);
-  else if (G) launch_eval<true, false, false>(a, B, lds, s, gv, scene->residual);
-  else if (S && T) launch_eval<false, true, true>(a, B, lds, s, gv, scene->residual);
-  else if (S) launch_eval<false, true, false>(a, B, lds, s, gv, scene->residual);
-  else if (T) launch_eval<false, false, true>(a, B, lds, s, gv, scene->residual);
-  else launch_eval<false, false, false>(a, B, lds, s, gv, scene->residual);
+  if (G && S && T) launch_eval<true, true, true>(a, B, lds, s, form, scene->residual);
+  else if (G && S) launch_eval<true, true, false>(a, B, lds, s, form, scene->residual);
+  else if (G && T) launch_eval<true, false, true>(a, B, lds, s, form, scene->residual);
+  else if (G) launch_eval<true, false, false>(a, B, lds, s, form, scene->residual);
+  else if (S && T) launch_eval<false, true, true>(a, B, lds, s, form, scene->residual);
+  else if (S) launch_eval<false, true, false>(a, B, lds, s, form, scene->residual);
+  else if (T) launch_eval<false, false, true>(a, B, lds, s, form, scene->residual);
+  else launch_eval<false, false, false>(a, B, lds, s, form, scene->residual);
   return hipGetLastError() == hipSuccess ? DAVA_OK : DAVA_ERR_LAUNCH;
 }
