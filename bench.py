@@ -709,7 +709,7 @@ def measurement_line(args, line, world, b, p, mn, distortion, ray, plan, kernel_
                 roofline["measured_ceiling"] = {
                     "ms": ceil[0], "GBps_history_reads": ceil[1],
                     "frac_of_measured_ceiling": round(ceil[0] / launch_ms, 4),
-                    "source": "tools/micro/solve_pass_stream 794 ceiling, run in this session after the timed "
+                    "source": "tools/micro/solve_pass_stream 794 ceiling (best of 8 launches), run in this session after the timed "
                               "region: the solve's own history pass over the same rows (B = 8192, 6 LDS-resident "
                               "entries, 512 problems resident), nothing else on the CU; frac = its time / the "
                               "solve's launch time"}

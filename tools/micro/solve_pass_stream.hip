@@ -60,23 +60,31 @@ void run(const char* tag, const float* hist, int B, int P, int Pv, int kcap, int
   const int lds = (8 * Pv + 2 * kcap + 2 * lcap * Pv) * 4;
   const auto k = solve_pass_kernel<GM, NW>;
   (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-  hipEvent_t a, b;
-  hipEventCreate(&a);
-  hipEventCreate(&b);
+  // one warm-up launch, then `reps` launches timed one by one: the best is the ceiling (boxes and runs
+  // differ by a few per cent; the mean is printed beside it)
   hipLaunchKernelGGL(k, dim3(B), dim3(64 * NW), lds, 0, hist, P, Pv, kcap, iters, lcap, out);
-  hipEventRecord(a);
-  const int reps = 5;
-  for (int r = 0; r < reps; ++r) hipLaunchKernelGGL(k, dim3(B), dim3(64 * NW), lds, 0, hist, P, Pv, kcap, iters, lcap, out);
-  hipEventRecord(b);
-  hipEventSynchronize(b);
-  float ms;
-  hipEventElapsedTime(&ms, a, b);
-  ms /= reps;
+  const int reps = 8;
+  float ms = 1e30f, mean = 0.f;
+  for (int r = 0; r < reps; ++r) {
+    hipEvent_t a, b;
+    (void)hipEventCreate(&a);
+    (void)hipEventCreate(&b);
+    (void)hipEventRecord(a);
+    hipLaunchKernelGGL(k, dim3(B), dim3(64 * NW), lds, 0, hist, P, Pv, kcap, iters, lcap, out);
+    (void)hipEventRecord(b);
+    (void)hipEventSynchronize(b);
+    float t;
+    (void)hipEventElapsedTime(&t, a, b);
+    ms = t < ms ? t : ms;
+    mean += t / reps;
+    (void)hipEventDestroy(a);
+    (void)hipEventDestroy(b);
+  }
   double entries = 0;  // entries read from HBM (the first lcap come from LDS)
   for (int it = 1; it <= iters; ++it) entries += (it < kcap ? it : kcap) > lcap ? (it < kcap ? it : kcap) - lcap : 0;
   const double bytes = entries * 2.0 * Pv * 4.0 * B;
-  printf("%-34s B=%5d P=%5d NW=%d lcap=%d lds=%6d: %8.3f ms  %7.1f GB/s  (%.1f GB/s per CU)\n", tag, B, P, NW, lcap, lds,
-         ms, bytes / ms / 1e6, bytes / ms / 1e6 / 256);
+  printf("%-34s B=%5d P=%5d NW=%d lcap=%d lds=%6d: %8.3f ms  %7.1f GB/s  (%.1f GB/s per CU; best of %d, mean %.3f ms)\n",
+         tag, B, P, NW, lcap, lds, ms, bytes / ms / 1e6, bytes / ms / 1e6 / 256, reps, mean);
 }
 }  // namespace micro
 
