@@ -54,8 +54,7 @@ struct SolveArgs {
   float* tape_s;  // (B, tape_T)
   int tape_T;
   int stagger;    // shader cycles per start level (0: none)
-  int stagger_levels;  // <= 1: odd workgroups wait `stagger`; L > 1: level (b >> stagger_shift) mod L waits level x stagger
-  int stagger_shift;
+  int stagger_levels;  // <= 1: odd workgroups wait `stagger`; L > 1: level (b / 8) mod L waits level x stagger
   float drop_p;   // training-mode drop path probability (0: eval mode)
   unsigned long long drop_seed;
   int second_last;  // training mode's return_second_last: a minimum-step stop keeps x_k
@@ -160,11 +159,6 @@ constexpr int kSolveWavesPerEU = 2;  // <= 256 VGPRs: two 4-wave workgroups per 
 // batch averages to stderr after the launch (and synchronises -- never in a product build).
 #ifndef DAVA_PHASE_TIMING
 #define DAVA_PHASE_TIMING 0
-#endif
-// A/B build switch (make variant FLAGS=-DDAVA_HIST_PREFETCH=1): the LDS-mode history pass issues its
-// first HBM batch before consuming the on-chip entries (compact_products_fused).
-#ifndef DAVA_HIST_PREFETCH
-#define DAVA_HIST_PREFETCH 0
 #endif
 #if DAVA_PHASE_TIMING
 constexpr int kPhases = 7;  // eval at x, history products, direction, trial evals, search logic, step, total
@@ -798,40 +792,21 @@ __device__ __forceinline__ void compact_products_fused(int P, int Pv, int nh, co
   };
   if constexpr (kHistDropsPrio<GM>) __builtin_amdgcn_s_setprio(kHistPrio);
   int j = wave;
-  const int nl = min(lcap, nh);
-  auto lds_entries = [&]() {  // on-chip entries first (wave-uniform)
-    for (; j < nl; j += NW) {
-      f4v s0[GM], w0[GM];
-      const float* sr = LH + (size_t)2 * j * Pv;
-      const float* wr = sr + Pv;
+  // on-chip entries first (wave-uniform).  (Rejected, r05, profiles/r05_ab_c2_stagger_prefetch.log,
+  // profiles/r05_ab_c3_prefetch.log: issuing the first HBM batch before consuming these, so its latency
+  // runs under them -- bitwise the same sums, C2 +0.1%, C3 -0.5%, 26 VGPRs spilled.)
+  for (const int nl = min(lcap, nh); j < nl; j += NW) {
+    f4v s0[GM], w0[GM];
+    const float* sr = LH + (size_t)2 * j * Pv;
+    const float* wr = sr + Pv;
 #pragma unroll
-      for (int m = 0; m < GM; ++m) {
-        const int q = lane + kWave * m;
-        s0[m] = ok[m] ? *reinterpret_cast<const f4v*>(sr + 4 * q) : f4v{0, 0, 0, 0};
-        w0[m] = ok[m] ? *reinterpret_cast<const f4v*>(wr + 4 * q) : f4v{0, 0, 0, 0};
-      }
-      consume(j, s0, w0);
+    for (int m = 0; m < GM; ++m) {
+      const int q = lane + kWave * m;
+      s0[m] = ok[m] ? *reinterpret_cast<const f4v*>(sr + 4 * q) : f4v{0, 0, 0, 0};
+      w0[m] = ok[m] ? *reinterpret_cast<const f4v*>(wr + 4 * q) : f4v{0, 0, 0, 0};
     }
-  };
-#if DAVA_HIST_PREFETCH
-  // The first HBM batch's loads are issued BEFORE the on-chip entries are consumed, so their latency
-  // runs under that work instead of after it.  The consumption order is unchanged (on-chip entries, then
-  // the batches in order): bitwise the same sums.
-  const int jh = nl > wave ? wave + (nl - wave + NW - 1) / NW * NW : wave;  // this wave's first HBM entry
-  if (nl > wave && jh + (EF - 1) * NW < nh) {
-    f4v s[EF][GM], w[EF][GM];
-#pragma unroll
-    for (int e = 0; e < EF; ++e) load(jh + e * NW, s[e], w[e]);
-    lds_entries();
-#pragma unroll
-    for (int e = 0; e < EF; ++e) consume(jh + e * NW, s[e], w[e]);
-    j = jh + EF * NW;
-  } else {
-    lds_entries();
+    consume(j, s0, w0);
   }
-#else
-  lds_entries();
-#endif
   // EF entries of this wave in flight: all loads issued before any is consumed.  (Rejected, r04,
   // profiles/r04_ab_variants_c2.log: two register batches, the next batch's loads issued before this
   // one is consumed -- C2 -2..-8%.)
@@ -924,8 +899,9 @@ __global__ __launch_bounds__(kWave * NW, kSolveWavesPerEU) void bfgs_ba_solve_ke
   // (workgroups are dealt round-robin, so b / 8 numbers them inside their XCD) the problems start at
   // L evenly spaced offsets.  Every problem alternates an HBM-bound history stream with a VALU-bound
   // objective evaluation; started together, all CUs stream at once and then all compute at once.
-  const int level = a.stagger_levels > 1 ? (int)((blockIdx.x >> a.stagger_shift) % (unsigned)a.stagger_levels)
-                                         : (blockIdx.x & 1);
+  // (Rejected, r05, profiles/r05_ab_c2_stagger_prefetch.log: levels by (b >> 8) mod L, i.e. the
+  // problems sharing one CU started a quarter or half of an iteration apart -- C2 within +-1%.)
+  const int level = a.stagger_levels > 1 ? (int)((blockIdx.x >> 3) % (unsigned)a.stagger_levels) : (blockIdx.x & 1);
   if (a.stagger > 0 && level > 0) {
     const unsigned long long t0 = clock64();
     const unsigned long long wait = (unsigned long long)a.stagger * (unsigned long long)level;
@@ -1515,10 +1491,10 @@ using namespace dava;
 
 // ---- debug overrides (dava_debug.hpp): set only through the two calls below, never from the environment ----
 namespace dava {
-static long long g_debug_knobs[kDbgKnobs] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};
+static long long g_debug_knobs[kDbgKnobs] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};
 static const char* const kDebugKnobNames[kDbgKnobs] = {
     "FORCE_GV", "GV_NO_XL", "SOLVE_WAVES", "WG_PER_CU", "LDS_HISTORY", "STAGGER", "STAGGER_LEVELS",
-    "NO_PPT", "NO_QUEUE", "ADJ_GV_WAVES", "ADJ_FORCE_GV", "ADJ_LDS_ENTRIES", "ADJ_GD_HBM", "STAGGER_SHIFT"};
+    "NO_PPT", "NO_QUEUE", "ADJ_GV_WAVES", "ADJ_FORCE_GV", "ADJ_LDS_ENTRIES", "ADJ_GD_HBM"};
 long long debug_knob(int k) { return k >= 0 && k < kDbgKnobs ? g_debug_knobs[k] : -1; }
 }  // namespace dava
 
@@ -1593,7 +1569,6 @@ static void launch_solve_ppt(const SolveArgs& a, int B, int lds, hipStream_t s) 
   args.stagger_levels = 1;
   if (debug_knob(kDbgStagger) >= 0) args.stagger = (int)debug_knob(kDbgStagger);  // A/B (cycles)
   if (debug_knob(kDbgStaggerLevels) >= 1) args.stagger_levels = (int)debug_knob(kDbgStaggerLevels);
-  args.stagger_shift = debug_knob(kDbgStaggerShift) >= 0 ? (int)debug_knob(kDbgStaggerShift) : 3;
   if (args.queue) {  // one workgroup per resident slot
     if (slots > 0) grid = min(B, slots);
     // The hardware already refills a slot as soon as its workgroup retires, but only from its
@@ -1714,7 +1689,6 @@ static int solve_impl(const DavaScene* scene, const DavaSolverConfig* config, co
   a.phase_cycles = nullptr;
   a.stagger = 0;
   a.stagger_levels = 1;
-  a.stagger_shift = 3;
   a.drop_p = config->drop_path_p;
   a.drop_seed = ((unsigned long long)config->drop_seed_hi << 32) | config->drop_seed_lo;
   a.second_last = config->return_second_last ? 1 : 0;

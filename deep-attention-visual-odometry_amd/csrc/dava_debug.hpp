@@ -23,7 +23,6 @@ enum DebugKnob : int {
   kDbgAdjForceGV,     // 1: global-vector-mode adjoint even where the LDS image fits
   kDbgAdjLdsEntries,  // >= 0: caps the adjoint's on-chip history entries
   kDbgAdjGdHbm,       // 1: the GV adjoint's dual gradient vector in HBM instead of LDS
-  kDbgStaggerShift,   // >= 0: multi-level stagger level = (workgroup >> this) mod levels (default 3)
   kDbgKnobs
 };
 

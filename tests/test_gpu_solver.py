@@ -5,7 +5,7 @@ Parity bar (north_star / SURVEY.md 8(d)): per-problem normwise
 The reference's own sensitivity to a 2-ulp input perturbation is ~1.4e-6 at
 K = 100, so 1e-5 leaves room for the different reduction
 order of the kernel.  Intrinsics (f, cx, cy) are also compared on their own,
-against max(1e-5, 10 x the oracle's own change under a 1-ulp nudge of x0):
+against max(1e-5, ENVELOPE_FACTOR x the oracle's own change under a 1-ulp nudge of x0):
 for a few ill-conditioned problems the reference itself moves f by more than
 1e-5 under such a nudge, and no fp32 implementation can be closer than that.
 """
@@ -22,7 +22,10 @@ pytestmark = pytest.mark.gpu
 
 TOL = 1e-5
 # Per-block envelopes: this many times the reference's own change under a 1-ulp nudge of x0 (floor TOL).
-ENVELOPE_FACTOR = 10.0
+# 4: the largest ratios measured past the 1e-5 floor are 3.65 (C5, dense, extrinsics block at K = 100,
+# profiles/r05_c5_parity_distribution.jsonl) and 3.03 (the headline's problem 39, distortion block,
+# profiles/r05_trace_intrinsics.jsonl; DESIGN 4.3 traces where it comes from).  Rounds 1-4 used 10.
+ENVELOPE_FACTOR = 4.0
 
 
 def _scene(b, m, n, distortion, seed):
@@ -57,7 +60,7 @@ def _rel(a, b):
 
 
 def _envelopes(x0, fn, ref, distortion=False, objective_of=None, **kw):
-    """Per-problem 10x the oracle's own change under a 1-ulp nudge of x0, up or down (floor
+    """Per-problem ENVELOPE_FACTOR x the oracle's own change under a 1-ulp nudge of x0, up or down (floor
     1e-5), for the whole parameter vector, for the intrinsics alone and (distortion) for the five
     Brown-Conrady coefficients alone.  Both directions: which side of a bifurcation a nudge lands
     on depends on the host CPU's torch kernels.  The distortion block is the least determined
@@ -68,10 +71,10 @@ def _envelopes(x0, fn, ref, distortion=False, objective_of=None, **kw):
     env_e = torch.full((b,), 1e-4, dtype=torch.float64)
     for to in (float("inf"), -float("inf")):
         nudged = solver.bfgs_solve(torch.nextafter(x0, torch.full_like(x0, to)), fn, **kw)
-        env = torch.maximum(env, 10.0 * _rel(nudged, ref))
-        env_i = torch.maximum(env_i, 10.0 * _rel(nudged[:, :3], ref[:, :3]))
+        env = torch.maximum(env, ENVELOPE_FACTOR * _rel(nudged, ref))
+        env_i = torch.maximum(env_i, ENVELOPE_FACTOR * _rel(nudged[:, :3], ref[:, :3]))
         if distortion:
-            env_d = torch.maximum(env_d, 10.0 * _rel(nudged[:, -5:], ref[:, -5:]))
+            env_d = torch.maximum(env_d, ENVELOPE_FACTOR * _rel(nudged[:, -5:], ref[:, -5:]))
         if objective_of is not None:  # the objective reached, relative: (E(nudged) - E(ref)) / E(ref)
             e_ref, e_n = objective_of(ref), objective_of(nudged)
             env_e = torch.maximum(env_e, torch.nan_to_num(10.0 * (e_n - e_ref).abs() / e_ref.abs(), nan=0.0))
@@ -106,7 +109,7 @@ def _report(tag, rel, env=None, extra=None):
 def _check_k100(out, ref, x0, obs, vis, m, n, distortion, env, env_intrinsics=None, tag=None):
     """Parity after K = 100 iterations, where small two-view problems run into fp32 stagnation.
 
-    Every problem must lie within max(1e-5, 10x the reference's own 1-ulp sensitivity) -- the
+    Every problem must lie within max(1e-5, ENVELOPE_FACTOR x the reference's own 1-ulp sensitivity) -- the
     envelope -- and within 1e-5 outright.  (Round 1 allowed one problem per case to fall back to an
     objective-value comparison, because two builds that differed only in FMA contraction each put a
     different single C1/C2 problem 1.6e-5 .. 4.2e-5 away at K = 100 -- a near-tie line-search branch
@@ -539,7 +542,7 @@ def test_ray_angle_golden_trajectories(device, case, ks, mode):
     """Against BFGSSolver().eval() of the REAL reference on CalibrationNetwork's error
     (tests/golden/ray_angle.npz).  The angle sum is not smooth where a residual vanishes,
     so later iterates are more sensitive than the squared objective's: every K is held to
-    max(1e-5, 10 x the reference's own change under a 1-ulp nudge of x0)."""
+    max(1e-5, ENVELOPE_FACTOR x the reference's own change under a 1-ulp nudge of x0)."""
     g = np.load(os.path.join(GOLDEN, "ray_angle.npz"))
     m, n = {"c1": (2, 64), "c2": (2, 128)}[case]
     key = f"traj_{case}"
@@ -800,6 +803,7 @@ def test_fused_second_last_matches_oracle(device):
     capped = rec.reason == solver.STOP_ITERATIONS
     assert int((~capped).sum()) >= 8
     assert torch.isfinite(out).all()
+    # (a foreign start is chaotic by construction: this case keeps the 10x factor of rounds 1-4)
     assert ((rel <= torch.clamp(10.0 * env, min=TOL)) | capped).all(), (rel, env, capped)
     # one problem at a time: always the fused kernel (a single problem cannot move rows)
     for i in range(4):
