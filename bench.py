@@ -48,7 +48,7 @@ import torch.distributed as dist  # noqa: E402
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 HBM_COPY_GBS = 6290.0  # measured float4 copy (MI355X_MICROARCH.md chip table: 79% of spec)
 PARITY_BAR = 1e-5  # north_star: converged params within 1e-5 rel of the reference
-ENVELOPE_FACTOR = 4.0  # per-block envelopes: max(1e-5, this x the oracle's own 1-ulp change) (tests: the same)
+ENVELOPE_FACTOR = 5.0  # per-block envelopes: max(1e-5, this x the oracle's own 1-ulp change) (tests: the same)
 
 
 def parse(argv=None):

@@ -65,13 +65,13 @@ def test_cpu_solve_matches_reference_c1_trajectories():
         if k < 100:
             assert (rel <= TOL).all(), (k, rel)
             continue
-        # K = 100: each problem inside max(1e-5, 4x the reference's own change under a 1-ulp nudge of x0)
+        # K = 100: each problem inside max(1e-5, 5x the reference's own change under a 1-ulp nudge of x0)
         oc = objective.ReprojectionClosure(obs, vis, 2, 64)
         env = torch.full((x0.shape[0],), TOL, dtype=torch.float64)
         for to in (float("inf"), -float("inf")):
             nudged = solver.bfgs_solve(torch.nextafter(x0, torch.full_like(x0, to)), oc, iterations=k,
                                        error_threshold=-1.0, minimum_step=-1.0)
-            env = torch.maximum(env, 4.0 * _rel(nudged, ref))
+            env = torch.maximum(env, 5.0 * _rel(nudged, ref))
         assert (rel <= env).all() and (rel <= TOL).all(), (rel, env)
 
 
