@@ -160,11 +160,6 @@ constexpr int kSolveWavesPerEU = 2;  // <= 256 VGPRs: two 4-wave workgroups per 
 #ifndef DAVA_PHASE_TIMING
 #define DAVA_PHASE_TIMING 0
 #endif
-// A/B build switch (make variant FLAGS=-DDAVA_GV_GROUP_RING=1): the staged GV history pass refills its
-// LDS stage group by group (wide_direction) instead of once per entry.
-#ifndef DAVA_GV_GROUP_RING
-#define DAVA_GV_GROUP_RING 0
-#endif
 #if DAVA_PHASE_TIMING
 constexpr int kPhases = 7;  // eval at x, history products, direction, trial evals, search logic, step, total
 #define DAVA_PHASE(i)                          \
@@ -527,54 +522,9 @@ __device__ __forceinline__ float wide_direction(int P, int Pv, int nh, const flo
       if (nh > 0) copy(0);
       const float* st_s = stage + 4 * tid;  // this thread's groups: + 4 u BLOCK floats
       const float* st_w = stage + Pv + 4 * tid;
-#if DAVA_GV_GROUP_RING
-      // Group-wise refill: group u of entry j + 1 is copied as soon as this thread has read group u of entry
-      // j back, so about one entry stays in flight all the time instead of draining while the whole entry
-      // is read back.  The copies retire in issue order; after group u's pair of entry j this wave issued
-      // the pairs of groups u + 1 .. GT - 1 of entry j and 0 .. u - 1 of entry j + 1: 2 (GT - 2) + 2 hl
-      // copies for every u < GT - 1 (hl: this wave has lanes in the last group), 2 (GT - 1) for u = GT - 1.
-      // The last entry waits for everything.  Same rows, same arithmetic: bitwise the one-shot refill.
-      const bool hl = __builtin_amdgcn_readfirstlane(tid / kWave) * kWave + (GT - 1) * BLOCK < G;
-      for (int j = 0; j < nh; ++j) {
-        f4v s4[GT], w4[GT];
-        const bool more = j + 1 < nh;
-        const unsigned long long sn = more ? uniform_ptr64(S + (size_t)(j + 1) * Pv) : 0ull;
-        const unsigned long long wn = more ? uniform_ptr64(W + (size_t)(j + 1) * Pv) : 0ull;
-#pragma unroll
-        for (int u = 0; u < GT; ++u) {
-          const int q = tid + u * BLOCK;
-          s4[u] = w4[u] = z;
-          if (u == GT - 1 && !hl) continue;  // (wave-uniform) no lane of this wave in the last group
-          if (!more) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          else if (u == GT - 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * (GT - 1)) : "memory");
-          else if (hl) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * (GT - 1)) : "memory");
-          else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * (GT - 2) > 0 ? 2 * (GT - 2) : 0) : "memory");
-          if (u < GT - 1 || q < G) {
-            s4[u] = *reinterpret_cast<const f4v*>(st_s + 4 * u * BLOCK);
-            w4[u] = *reinterpret_cast<const f4v*>(st_w + 4 * u * BLOCK);
-          }
-          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // read back before the copy overwrites it
-          if (more && q < G) {
-            const unsigned ds = __builtin_amdgcn_readfirstlane(stage_off + 16u * (unsigned)(u * BLOCK));
-            const unsigned dw = __builtin_amdgcn_readfirstlane(ds + w_bytes);
-            const unsigned long long su = sn + 16ull * (unsigned long long)(u * BLOCK);
-            const unsigned long long wu = wn + 16ull * (unsigned long long)(u * BLOCK);
-            unsigned saved;
-            asm volatile(
-                "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\t"
-                "s_mov_b32 m0, %0"
-                : "=&s"(saved)
-                : "v"(voff), "s"(su), "s"(ds)
-                : "memory");
-            asm volatile(
-                "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\t"
-                "s_mov_b32 m0, %0"
-                : "=&s"(saved)
-                : "v"(voff), "s"(wu), "s"(dw)
-                : "memory");
-          }
-        }
-#else
+// (Rejected, r05, profiles/r05_ab_c5_group_ring_rejected.log: refilling the stage group by group -- group
+      // u of entry j + 1 copied as soon as group u of entry j is read back, explicit vmcnt per group -- so
+      // about one entry stays in flight while the entry is read back: bitwise the same, C5 -0.6%.)
       for (int j = 0; j < nh; ++j) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this thread's copies of entry j have landed
         f4v s4[GT], w4[GT];
@@ -589,7 +539,6 @@ __device__ __forceinline__ float wide_direction(int P, int Pv, int nh, const flo
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // read back before the next copy overwrites it
         if (j + 1 < nh) copy(j + 1);
-#endif
         f2v sy2 = {0.f, 0.f}, wy2 = {0.f, 0.f}, sg2 = {0.f, 0.f}, wg2 = {0.f, 0.f};
 #pragma unroll
         for (int u = 0; u < GT; ++u) {
