@@ -721,7 +721,7 @@ def measurement_line(args, line, world, b, p, mn, distortion, ray, plan, kernel_
             roofline["traffic_over_algorithmic"] = round(measured / algo, 4)
         else:
             roofline["traffic_live_failed"] = detail
-        if headline:
+        if headline and args.mode == "compact":
             ceil = live_ceiling(p)
             if ceil is not None:
                 roofline["measured_ceiling"] = {
