@@ -13,6 +13,7 @@ run() {
 }
 run C2_b64 --batch 64 --views 2 --points 128 --no-distortion &&
 run C2_b256 --batch 256 --views 2 --points 128 --no-distortion &&
+run C2_b512 --batch 512 --views 2 --points 128 --no-distortion &&
 run C2 --batch 1024 --views 2 --points 128 --no-distortion &&
 run C3 &&
 run C5 --batch 256 --views 16 --points 4096 --no-distortion
