@@ -701,6 +701,8 @@ constexpr bool kHistDropsPrio = GM <= 2;
 // is consumed (a register ring) -- at the 256-VGPR cap the spills (scratch ops 26 -> 201) cost C3 33%,
 // C2 13% (profiles/r02_ab_history_ring.log).
 template <int GM>
+constexpr bool kBatchAllEntries = GM <= 2;  // compact_products_fused: on-chip entries in batches too
+template <int GM>
 __host__ __device__ constexpr int fused_inflight() {
   return GM <= 2 ? 4 : 2;  // rows of <= 2 float4 groups per lane (P <= 512: C1, C2) : 3-4 groups (C3)
 }
@@ -795,6 +797,45 @@ __device__ __forceinline__ void compact_products_fused(int P, int Pv, int nh, co
   };
   if constexpr (kHistDropsPrio<GM>) __builtin_amdgcn_s_setprio(kHistPrio);
   int j = wave;
+  if constexpr (kBatchAllEntries<GM>) {
+  // Rows of <= 2 groups (C1, C2): the on-chip entries and the HBM remainder go through batches too (up to
+  // EF entries loaded, then consumed in order), so their consume chains (dots, wave reduction,
+  // coefficients, accumulation) interleave instead of running one entry at a time.  Same entries in the
+  // same order: bitwise the one-at-a-time form (profiles/r05_ab_batch_serial.log: 1024 / 1024 C2 and
+  // 2048 / 2048 C3 rows equal; C1 shape +1.2%, C2 at B = 256 +1.1%, C2 at B = 1024 +-0; rows of 4 groups,
+  // C3: -0.7%, so they keep the one-at-a-time form).
+  auto lds_load = [&](int jj, f4v (&s4)[GM], f4v (&w4)[GM]) {
+    const float* sr = LH + (size_t)2 * jj * Pv;
+    const float* wr = sr + Pv;
+#pragma unroll
+    for (int m = 0; m < GM; ++m) {
+      const int q = lane + kWave * m;
+      s4[m] = ok[m] ? *reinterpret_cast<const f4v*>(sr + 4 * q) : f4v{0, 0, 0, 0};
+      w4[m] = ok[m] ? *reinterpret_cast<const f4v*>(wr + 4 * q) : f4v{0, 0, 0, 0};
+    }
+  };
+  auto batch = [&](auto count, int jj, auto&& loader) {
+    constexpr int C = decltype(count)::value;
+    f4v s[C][GM], w[C][GM];
+#pragma unroll
+    for (int e = 0; e < C; ++e) loader(jj + e * NW, s[e], w[e]);
+#pragma unroll
+    for (int e = 0; e < C; ++e) consume(jj + e * NW, s[e], w[e]);
+  };
+  auto batch_of = [&](int cnt, int jj, auto&& loader) {  // cnt: 1 .. EF, wave-uniform
+    if (cnt >= 4 && EF >= 4) batch(std::integral_constant<int, (EF >= 4 ? 4 : 1)>{}, jj, loader);
+    else if (cnt == 3 && EF >= 3) batch(std::integral_constant<int, (EF >= 3 ? 3 : 1)>{}, jj, loader);
+    else if (cnt >= 2) batch(std::integral_constant<int, 2>{}, jj, loader);
+    else batch(std::integral_constant<int, 1>{}, jj, loader);
+  };
+  for (const int nl = min(lcap, nh); j < nl;) {
+    const int cnt = min(EF, (nl - j + NW - 1) / NW);
+    batch_of(cnt, j, lds_load);
+    j += cnt * NW;
+  }
+  for (; j + (EF - 1) * NW < nh; j += EF * NW) batch(std::integral_constant<int, EF>{}, j, load);
+  if (j < nh) batch_of((nh - j + NW - 1) / NW, j, load);
+  } else {
   // on-chip entries first (wave-uniform).  (Rejected, r05, profiles/r05_ab_c2_stagger_prefetch.log,
   // profiles/r05_ab_c3_prefetch.log: issuing the first HBM batch before consuming these, so its latency
   // runs under them -- bitwise the same sums, C2 +0.1%, C3 -0.5%, 26 VGPRs spilled.)
@@ -824,6 +865,7 @@ __device__ __forceinline__ void compact_products_fused(int P, int Pv, int nh, co
     f4v s0[GM], w0[GM];
     load(j, s0, w0);
     consume(j, s0, w0);
+  }
   }
   if constexpr (kHistDropsPrio<GM>) __builtin_amdgcn_s_setprio(kBasePrio);
   // deterministic cross-wave sum: ((w0 + w2) + (w1 + w3)) + gamma0 * (y | g)  (NW = 4),
