@@ -1,0 +1,107 @@
+// Microbenchmark (not part of the library): the global-vector solve's history pass alone --
+// dava::wide_direction<GT, 8, STAGED> from csrc/bfgs_solve.hip (C5: P = 12,381, GT = 7 float4 groups per
+// thread, eight waves, one workgroup per problem) -- run back to back over a history that grows by one
+// entry per "iteration", as the solve does, with nothing else on the CU.  STAGED = the solve's XL form
+// (rows HBM -> LDS by global_load_lds one entry ahead); otherwise the rows go to registers.  B = 1 / 16
+// / 256 workgroups: one CU alone, a few, every CU.  Prints ms and GB/s of history rows read, and the time
+// per entry.  The question it answers: what bounds the C5 history phase (≈ 4.6 us per 99 KB entry in
+// the solve at B = 256).
+// build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -fno-slp-vectorize -I../../include
+//        -I../../deep-attention-visual-odometry_amd/csrc wide_pass_stream.hip -o wide_pass_stream
+#include "../../deep-attention-visual-odometry_amd/csrc/bfgs_solve.hip"
+
+#include <cstdio>
+#include <cstdlib>
+
+namespace micro {
+using namespace dava;
+
+constexpr int kNW = 8;
+constexpr int kGT = 7;
+
+// per problem in HBM: S rows, W rows (kcap x Pv each), then g, gp, s vectors (Pv each)
+template <bool STAGED>
+__global__ __launch_bounds__(64 * kNW, 1) void wide_kernel(float* __restrict__ ws, int P, int Pv, int kcap,
+                                                           int iters, float* out) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  float* d = lds;                 // Pv (XL: d slot), followed by the gradient slot: the stage (2 Pv)
+  float* hrho = lds + 2 * Pv;     // kcap
+  float* hc = hrho + kcap;        // kcap
+  float* scratch = hc + kcap;     // 2 * NW * 32
+  float* S = ws + (size_t)blockIdx.x * (2 * (size_t)kcap * Pv + 3 * (size_t)Pv);
+  float* W = S + (size_t)kcap * Pv;
+  float* g = W + (size_t)kcap * Pv;
+  float* gp = g + Pv;
+  float* s = gp + Pv;
+  for (int i = threadIdx.x; i < kcap; i += 64 * kNW) { hrho[i] = 0.5f; hc[i] = 1.25f; }
+  __syncthreads();
+  int buf = 0;
+  float acc = 0.f;
+  for (int it = 1; it <= iters; ++it) {
+    const int nh = it - 1 < kcap ? it - 1 : kcap - 1;
+    // appends go to entry nh (rewritten every iteration once the history is full)
+    acc += wide_direction<kGT, kNW, STAGED>(P, Pv, nh, S, W, hrho, hc, 1.0f, g, gp, s, d, S + (size_t)nh * Pv,
+                                            W + (size_t)nh * Pv, scratch, buf, nh, nullptr, nullptr,
+                                            STAGED ? lds : nullptr);
+    __syncthreads();
+  }
+  if (acc == 12345.f) out[blockIdx.x] = acc;  // keep the work
+}
+
+__global__ void fill(float* p, size_t n) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    p[i] = 1e-4f * (float)((i * 2654435761u) % 1000u) - 0.05f;
+}
+
+template <bool STAGED>
+void run(const char* tag, float* ws, int B, int P, int Pv, int kcap, int iters, float* out) {
+  const int lds = (2 * Pv + 2 * kcap + 2 * kNW * 32) * 4;
+  const auto k = wide_kernel<STAGED>;
+  (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+  hipLaunchKernelGGL(k, dim3(B), dim3(64 * kNW), lds, 0, ws, P, Pv, kcap, iters, out);
+  const int reps = 3;
+  float best = 1e30f;
+  for (int r = 0; r < reps; ++r) {
+    hipEvent_t a, b;
+    (void)hipEventCreate(&a);
+    (void)hipEventCreate(&b);
+    (void)hipEventRecord(a);
+    hipLaunchKernelGGL(k, dim3(B), dim3(64 * kNW), lds, 0, ws, P, Pv, kcap, iters, out);
+    (void)hipEventRecord(b);
+    (void)hipEventSynchronize(b);
+    float t;
+    (void)hipEventElapsedTime(&t, a, b);
+    best = t < best ? t : best;
+    (void)hipEventDestroy(a);
+    (void)hipEventDestroy(b);
+  }
+  double entries = 0;
+  for (int it = 1; it <= iters; ++it) entries += it - 1 < kcap ? it - 1 : kcap - 1;
+  const double bytes = entries * 2.0 * Pv * 4.0 * B;
+  printf("%-22s B=%4d P=%5d: %8.3f ms  %7.1f GB/s  (%.1f GB/s per CU in use; %.2f us per entry)\n", tag, B, P, best,
+         bytes / best / 1e6, bytes / best / 1e6 / (B < 256 ? B : 256), best * 1e3 / entries);
+}
+}  // namespace micro
+
+int main(int argc, char** argv) {
+  const int P = argc > 1 ? atoi(argv[1]) : 12381;  // C5: 16 views x 4096 points
+  const int iters = 100, kcap = 99;
+  const int Pv = (P + 3) / 4 * 4;
+  if ((Pv / 4 + 511) / 512 != micro::kGT) {
+    printf("P = %d needs %d groups per thread, this build has %d\n", P, (Pv / 4 + 511) / 512, micro::kGT);
+    return 1;
+  }
+  const int Bmax = 256;
+  float *ws, *out;
+  const size_t per = 2 * (size_t)kcap * Pv + 3 * (size_t)Pv;
+  if (hipMalloc(&ws, Bmax * per * 4) != hipSuccess || hipMalloc(&out, Bmax * 4) != hipSuccess) return 1;
+  hipLaunchKernelGGL(micro::fill, dim3(4096), dim3(256), 0, 0, ws, Bmax * per);
+  for (int B : {1, 16, 64, 256}) {
+    micro::run<true>("staged (XL form)", ws, B, P, Pv, kcap, iters, out);
+    micro::run<false>("registers", ws, B, P, Pv, kcap, iters, out);
+  }
+  if (hipDeviceSynchronize() != hipSuccess) return 1;
+  hipFree(ws);
+  hipFree(out);
+  return 0;
+}
