@@ -90,7 +90,10 @@ __host__ __device__ constexpr int solve_waves(bool gv) { return gv ? 8 : 4; }
 constexpr int kWideMaxGroups = 7;
 // History entries per block reduction in the wide pass for rows of > 2 groups per thread (two
 // entries' rows do not fit the registers beside y, g and the sums there).
-constexpr int kGvEntries = 1;
+#ifndef DAVA_GV_ENTRIES
+#define DAVA_GV_ENTRIES 1  // (microbenchmark builds only: tools/micro/wide_pass_stream.hip)
+#endif
+constexpr int kGvEntries = DAVA_GV_ENTRIES;
 __host__ __device__ inline bool wide_history_pass(int Pv, int kcap, bool gv) {
   return gv && kcap > 0 && (Pv / 4 + kWave * solve_waves(gv) - 1) / (kWave * solve_waves(gv)) <= kWideMaxGroups;
 }
@@ -444,14 +447,16 @@ __device__ __forceinline__ void compact_products_wide(int P, int Pv, int nh, con
 // the spills cost 14% with one entry and 19% with two.  Forming only H'g from the history and
 // H'y = H'g + d_prev: two entries per reduction, +0.5..0.9% at C5 but a different rounding that moved
 // a C2 problem 2.1e-5 from the oracle, profiles/r03_ab_hy_from_d.log.)
-template <int GT, int NW, bool STAGED = false>
+template <int GT, int NW, bool STAGED = false, int ROWSLOTS = 2>
 __device__ __forceinline__ float wide_direction(int P, int Pv, int nh, const float* __restrict__ S,
                                                 const float* __restrict__ W, float* hrho, float* hc, float gamma0,
                                                 const float* g, const float* gp, const float* s_cur, float* d,
                                                 float* s_row, float* w_row, float* scratch, int& buf, int entry,
-                                                float* tape_rho, float* tape_c, float* stage = nullptr) {
+                                                float* tape_rho, float* tape_c, float* stage = nullptr,
+                                                size_t row_stride = 0) {
   constexpr int BLOCK = kWave * NW;
   constexpr int E = GT <= 2 ? 2 : kGvEntries;
+  const size_t RSd = row_stride ? row_stride : (size_t)Pv;  // floats from one history row to the next
   const int tid = threadIdx.x;
   const int G = (P + 3) / 4;
   const f4v z = f4v{0, 0, 0, 0};
@@ -493,40 +498,47 @@ __device__ __forceinline__ float wide_direction(int P, int Pv, int nh, const flo
       };
       const unsigned w_bytes = __builtin_amdgcn_readfirstlane(4u * (unsigned)Pv);
       const unsigned voff = 16u * (unsigned)tid;  // one VGPR for every group: the group's step is in the base
-      auto copy = [&](int jj) {  // entry jj's S row -> stage[0, Pv), W row -> stage[Pv, 2 Pv), own groups
+      // The stage holds ROWSLOTS rows (Pv floats each; the solve's XL image has room for 2, one entry): the
+      // rows stream as S_0, W_0, S_1, W_1, ..., row r into slot r % ROWSLOTS, each issued as soon as the row
+      // ROWSLOTS before it (same slot) has been read back.  ROWSLOTS = 2 is one entry: entry j + 1 copied
+      // while entry j is consumed.
+      const int nrows = 2 * nh;
+      auto copy_row = [&](int r) {  // row r (entry r / 2, S or W) -> slot r % ROWSLOTS, this thread's groups
+        const float* row = ((r & 1) ? W : S) + (size_t)(r >> 1) * RSd;
+        const unsigned slot_off = __builtin_amdgcn_readfirstlane(4u * (unsigned)Pv * (unsigned)(r % ROWSLOTS));
 #pragma unroll
         for (int u = 0; u < GT; ++u) {
           const int q = tid + u * BLOCK;
-          const unsigned long long srow_u = uniform_ptr64(S + (size_t)jj * Pv + 4 * u * BLOCK);
-          const unsigned long long wrow_u = uniform_ptr64(W + (size_t)jj * Pv + 4 * u * BLOCK);
-          const unsigned ds = __builtin_amdgcn_readfirstlane(stage_off + 16u * (unsigned)(u * BLOCK));
-          const unsigned dw = __builtin_amdgcn_readfirstlane(ds + w_bytes);
+          const unsigned long long row_u = uniform_ptr64(row + 4 * u * BLOCK);
+          const unsigned ds = __builtin_amdgcn_readfirstlane(stage_off + slot_off + 16u * (unsigned)(u * BLOCK));
           if (q < G) {
             unsigned saved;
             asm volatile(
                 "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\t"
                 "s_mov_b32 m0, %0"
                 : "=&s"(saved)
-                : "v"(voff), "s"(srow_u), "s"(ds)
-                : "memory");
-            asm volatile(
-                "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\t"
-                "s_mov_b32 m0, %0"
-                : "=&s"(saved)
-                : "v"(voff), "s"(wrow_u), "s"(dw)
+                : "v"(voff), "s"(row_u), "s"(ds)
                 : "memory");
           }
         }
       };
       (void)lane_off;
-      if (nh > 0) copy(0);
-      const float* st_s = stage + 4 * tid;  // this thread's groups: + 4 u BLOCK floats
-      const float* st_w = stage + Pv + 4 * tid;
-// (Rejected, r05, profiles/r05_ab_c5_group_ring_rejected.log: refilling the stage group by group -- group
-      // u of entry j + 1 copied as soon as group u of entry j is read back, explicit vmcnt per group -- so
-      // about one entry stays in flight while the entry is read back: bitwise the same, C5 -0.6%.)
+      (void)w_bytes;
+#pragma unroll
+      for (int r = 0; r < ROWSLOTS; ++r)
+        if (r < nrows) copy_row(r);
+      // (the last group's copies are issued only by waves with lanes in it)
+      const bool hl = __builtin_amdgcn_readfirstlane(tid / kWave) * kWave + (GT - 1) * BLOCK < G;
       for (int j = 0; j < nh; ++j) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this thread's copies of entry j have landed
+        // rows 2j and 2j + 1 must have landed; rows issued after them may stay in flight
+        if (ROWSLOTS > 2 && 2 * j + 2 < nrows) {
+          if (hl) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GT * (ROWSLOTS - 2)) : "memory");
+          else asm volatile("s_waitcnt vmcnt(%0)" ::"n"((GT - 1) * (ROWSLOTS - 2)) : "memory");
+        } else {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this thread's copies of entry j have landed
+        }
+        const float* st_s = stage + Pv * ((2 * j) % ROWSLOTS) + 4 * tid;  // this thread's groups: + 4 u BLOCK
+        const float* st_w = stage + Pv * ((2 * j + 1) % ROWSLOTS) + 4 * tid;
         f4v s4[GT], w4[GT];
 #pragma unroll
         for (int u = 0; u < GT; ++u) {
@@ -537,8 +549,9 @@ __device__ __forceinline__ float wide_direction(int P, int Pv, int nh, const flo
             w4[u] = *reinterpret_cast<const f4v*>(st_w + 4 * u * BLOCK);
           }
         }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // read back before the next copy overwrites it
-        if (j + 1 < nh) copy(j + 1);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // read back before the next copies overwrite it
+        if (2 * j + ROWSLOTS < nrows) copy_row(2 * j + ROWSLOTS);
+        if (2 * j + 1 + ROWSLOTS < nrows) copy_row(2 * j + 1 + ROWSLOTS);
         f2v sy2 = {0.f, 0.f}, wy2 = {0.f, 0.f}, sg2 = {0.f, 0.f}, wg2 = {0.f, 0.f};
 #pragma unroll
         for (int u = 0; u < GT; ++u) {
@@ -548,8 +561,12 @@ __device__ __forceinline__ float wide_direction(int P, int Pv, int nh, const flo
           wg2 = pk_fma(w4[u].lo, gg[u].lo, wg2); wg2 = pk_fma(w4[u].hi, gg[u].hi, wg2);
         }
         float dd[4] = {sy2.x + sy2.y, wy2.x + wy2.y, sg2.x + sg2.y, wg2.x + wg2.y};
+#if DAVA_MICRO_NOSYNC  // (tools/micro/wide_pass_stream.hip only: the wave's own partial dots, no barrier -- timing)
+        wave_sums<4>(dd);
+#else
         block_sum<4, NW, true>(dd, scratch, buf);
         buf ^= 1;
+#endif
         const float rho = hrho[j], cr = hc[j] * rho;
         const float ay = fmaf(cr, dd[0], -(rho * dd[1])), by = -rho * dd[0];
         const float ag = fmaf(cr, dd[2], -(rho * dd[3])), bg = -rho * dd[2];
@@ -571,14 +588,14 @@ __device__ __forceinline__ float wide_direction(int P, int Pv, int nh, const flo
       for (int u = 0; u < GT; ++u) {
         const int q = tid + u * BLOCK;
         if (u < GT - 1 && (E == 1 || e < ne)) {  // groups 0 .. GT-2 lie inside the row for every thread
-          s4[e][u] = *reinterpret_cast<const f4v*>(S + (size_t)(j + e) * Pv + 4 * q);
-          w4[e][u] = *reinterpret_cast<const f4v*>(W + (size_t)(j + e) * Pv + 4 * q);
+          s4[e][u] = *reinterpret_cast<const f4v*>(S + (size_t)(j + e) * RSd + 4 * q);
+          w4[e][u] = *reinterpret_cast<const f4v*>(W + (size_t)(j + e) * RSd + 4 * q);
           continue;
         }
         s4[e][u] = w4[e][u] = z;
         if (e < ne && q < G) {
-          s4[e][u] = *reinterpret_cast<const f4v*>(S + (size_t)(j + e) * Pv + 4 * q);
-          w4[e][u] = *reinterpret_cast<const f4v*>(W + (size_t)(j + e) * Pv + 4 * q);
+          s4[e][u] = *reinterpret_cast<const f4v*>(S + (size_t)(j + e) * RSd + 4 * q);
+          w4[e][u] = *reinterpret_cast<const f4v*>(W + (size_t)(j + e) * RSd + 4 * q);
         }
       }
     }

@@ -2,7 +2,8 @@
 // dava::wide_direction<GT, 8, STAGED> from csrc/bfgs_solve.hip (C5: P = 12,381, GT = 7 float4 groups per
 // thread, eight waves, one workgroup per problem) -- run back to back over a history that grows by one
 // entry per "iteration", as the solve does, with nothing else on the CU.  STAGED = the solve's XL form
-// (rows HBM -> LDS by global_load_lds one entry ahead); otherwise the rows go to registers.  B = 1 / 16
+// (rows HBM -> LDS by global_load_lds one entry ahead; with 3 row slots 1.5 entries ahead, the LDS the
+// solve's x would have to give up); otherwise the rows go to registers.  B = 1 / 16
 // / 256 workgroups: one CU alone, a few, every CU.  Prints ms and GB/s of history rows read, and the time
 // per entry.  The question it answers: what bounds the C5 history phase (≈ 4.6 us per 99 KB entry in
 // the solve at B = 256).
@@ -20,17 +21,28 @@ constexpr int kNW = 8;
 constexpr int kGT = 7;
 
 // per problem in HBM: S rows, W rows (kcap x Pv each), then g, gp, s vectors (Pv each)
-template <bool STAGED>
+// layout 0: per problem [S rows | W rows | g gp s], problems `stride` floats apart;
+// layout 1 (entry-major): S row j of problem b at (j B + b) Pv, W rows after all S rows, vectors after those
+template <bool STAGED, int RS>
 __global__ __launch_bounds__(64 * kNW, 1) void wide_kernel(float* __restrict__ ws, int P, int Pv, int kcap,
-                                                           int iters, float* out) {
+                                                           int iters, float* out, size_t stride, int layout) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
-  float* d = lds;                 // Pv (XL: d slot), followed by the gradient slot: the stage (2 Pv)
-  float* hrho = lds + 2 * Pv;     // kcap
+  float* d = lds;                 // the stage: RS rows (Pv each; the solve's XL form: d and the gradient slot)
+  float* hrho = lds + RS * Pv;    // kcap
   float* hc = hrho + kcap;        // kcap
   float* scratch = hc + kcap;     // 2 * NW * 32
-  float* S = ws + (size_t)blockIdx.x * (2 * (size_t)kcap * Pv + 3 * (size_t)Pv);
-  float* W = S + (size_t)kcap * Pv;
-  float* g = W + (size_t)kcap * Pv;
+  float *S, *W, *g;
+  size_t rs = Pv;  // row stride
+  if (layout == 0) {
+    S = ws + (size_t)blockIdx.x * stride;
+    W = S + (size_t)kcap * Pv;
+    g = W + (size_t)kcap * Pv;
+  } else {
+    S = ws + (size_t)blockIdx.x * Pv;
+    W = ws + (size_t)kcap * gridDim.x * Pv + (size_t)blockIdx.x * Pv;
+    g = ws + 2 * (size_t)kcap * gridDim.x * Pv + (size_t)blockIdx.x * 3 * Pv;
+    rs = (size_t)gridDim.x * Pv;
+  }
   float* gp = g + Pv;
   float* s = gp + Pv;
   for (int i = threadIdx.x; i < kcap; i += 64 * kNW) { hrho[i] = 0.5f; hc[i] = 1.25f; }
@@ -40,9 +52,9 @@ __global__ __launch_bounds__(64 * kNW, 1) void wide_kernel(float* __restrict__ w
   for (int it = 1; it <= iters; ++it) {
     const int nh = it - 1 < kcap ? it - 1 : kcap - 1;
     // appends go to entry nh (rewritten every iteration once the history is full)
-    acc += wide_direction<kGT, kNW, STAGED>(P, Pv, nh, S, W, hrho, hc, 1.0f, g, gp, s, d, S + (size_t)nh * Pv,
-                                            W + (size_t)nh * Pv, scratch, buf, nh, nullptr, nullptr,
-                                            STAGED ? lds : nullptr);
+    acc += wide_direction<kGT, kNW, STAGED, RS>(P, Pv, nh, S, W, hrho, hc, 1.0f, g, gp, s, d, S + (size_t)nh * rs,
+                                                W + (size_t)nh * rs, scratch, buf, nh, nullptr, nullptr,
+                                                STAGED ? lds : nullptr, rs);
     __syncthreads();
   }
   if (acc == 12345.f) out[blockIdx.x] = acc;  // keep the work
@@ -53,12 +65,12 @@ __global__ void fill(float* p, size_t n) {
     p[i] = 1e-4f * (float)((i * 2654435761u) % 1000u) - 0.05f;
 }
 
-template <bool STAGED>
-void run(const char* tag, float* ws, int B, int P, int Pv, int kcap, int iters, float* out) {
-  const int lds = (2 * Pv + 2 * kcap + 2 * kNW * 32) * 4;
-  const auto k = wide_kernel<STAGED>;
+template <bool STAGED, int RS = 2>
+void run(const char* tag, float* ws, int B, int P, int Pv, int kcap, int iters, float* out, size_t stride, int layout) {
+  const int lds = (RS * Pv + 2 * kcap + 2 * kNW * 32) * 4;
+  const auto k = wide_kernel<STAGED, RS>;
   (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-  hipLaunchKernelGGL(k, dim3(B), dim3(64 * kNW), lds, 0, ws, P, Pv, kcap, iters, out);
+  hipLaunchKernelGGL(k, dim3(B), dim3(64 * kNW), lds, 0, ws, P, Pv, kcap, iters, out, stride, layout);
   const int reps = 3;
   float best = 1e30f;
   for (int r = 0; r < reps; ++r) {
@@ -66,7 +78,7 @@ void run(const char* tag, float* ws, int B, int P, int Pv, int kcap, int iters, 
     (void)hipEventCreate(&a);
     (void)hipEventCreate(&b);
     (void)hipEventRecord(a);
-    hipLaunchKernelGGL(k, dim3(B), dim3(64 * kNW), lds, 0, ws, P, Pv, kcap, iters, out);
+    hipLaunchKernelGGL(k, dim3(B), dim3(64 * kNW), lds, 0, ws, P, Pv, kcap, iters, out, stride, layout);
     (void)hipEventRecord(b);
     (void)hipEventSynchronize(b);
     float t;
@@ -94,11 +106,18 @@ int main(int argc, char** argv) {
   const int Bmax = 256;
   float *ws, *out;
   const size_t per = 2 * (size_t)kcap * Pv + 3 * (size_t)Pv;
-  if (hipMalloc(&ws, Bmax * per * 4) != hipSuccess || hipMalloc(&out, Bmax * 4) != hipSuccess) return 1;
-  hipLaunchKernelGGL(micro::fill, dim3(4096), dim3(256), 0, 0, ws, Bmax * per);
-  for (int B : {1, 16, 64, 256}) {
-    micro::run<true>("staged (XL form)", ws, B, P, Pv, kcap, iters, out);
-    micro::run<false>("registers", ws, B, P, Pv, kcap, iters, out);
+  const size_t pad = 3328;  // floats: 13 KB, an odd multiple of 256 B
+  if (hipMalloc(&ws, Bmax * (per + pad) * 4) != hipSuccess || hipMalloc(&out, Bmax * 4) != hipSuccess) return 1;
+  hipLaunchKernelGGL(micro::fill, dim3(4096), dim3(256), 0, 0, ws, Bmax * (per + pad));
+  for (int B : {1, 64, 256}) {
+#if DAVA_MICRO_NOSYNC
+    micro::run<true, 2>("staged, NO block sum", ws, B, P, Pv, kcap, iters, out, per, 0);
+    continue;
+#endif
+    micro::run<true, 2>("staged, problem-major", ws, B, P, Pv, kcap, iters, out, per, 0);
+    micro::run<true, 2>("staged, padded stride", ws, B, P, Pv, kcap, iters, out, per + pad, 0);
+    micro::run<true, 2>("staged, entry-major", ws, B, P, Pv, kcap, iters, out, per, 1);
+    if (B == 256) micro::run<false>("registers, entry-major", ws, B, P, Pv, kcap, iters, out, per, 1);
   }
   if (hipDeviceSynchronize() != hipSuccess) return 1;
   hipFree(ws);
