@@ -97,7 +97,8 @@ void run(const char* tag, float* ws, int B, int P, int Pv, int kcap, int iters, 
 
 int main(int argc, char** argv) {
   const int P = argc > 1 ? atoi(argv[1]) : 12381;  // C5: 16 views x 4096 points
-  const int iters = 100, kcap = 99;
+  // argv[2]: iterations (the history's footprint: 2 (iters - 1) Pv floats per problem), default the solve's 100
+  const int iters = argc > 2 ? atoi(argv[2]) : 100, kcap = iters - 1;
   const int Pv = (P + 3) / 4 * 4;
   if ((Pv / 4 + 511) / 512 != micro::kGT) {
     printf("P = %d needs %d groups per thread, this build has %d\n", P, (Pv / 4 + 511) / 512, micro::kGT);
@@ -109,6 +110,11 @@ int main(int argc, char** argv) {
   const size_t pad = 3328;  // floats: 13 KB, an odd multiple of 256 B
   if (hipMalloc(&ws, Bmax * (per + pad) * 4) != hipSuccess || hipMalloc(&out, Bmax * 4) != hipSuccess) return 1;
   hipLaunchKernelGGL(micro::fill, dim3(4096), dim3(256), 0, 0, ws, Bmax * (per + pad));
+  if (argc > 2) {  // footprint scan: B = 256 only
+    micro::run<true, 2>("staged, problem-major", ws, 256, P, Pv, kcap, iters, out, per, 0);
+    micro::run<false>("registers", ws, 256, P, Pv, kcap, iters, out, per, 0);
+    return hipDeviceSynchronize() == hipSuccess ? 0 : 1;
+  }
   for (int B : {1, 64, 256}) {
 #if DAVA_MICRO_NOSYNC
     micro::run<true, 2>("staged, NO block sum", ws, B, P, Pv, kcap, iters, out, per, 0);
