@@ -41,6 +41,7 @@ struct SolveArgs {
   float* err_out;
   int32_t* status;
   float* hess;
+  float* hess_dense;  // HYBRID: B x P x Pld dense matrices after the histories (else null)
   float c1, c2, thr, min_step;
   int iters, max_trials, strong, mode;
   int kcap;       // COMPACT: history capacity (entries)
@@ -258,6 +259,73 @@ __device__ __forceinline__ void dense_sweep(const Layout& L, int Pld, float* __r
     if (act) {
       st4(hy_out + j0, make_float4(ay[0], ay[1], ay[2], ay[3]));
       st4(hg_out + j0, make_float4(ag[0], ag[1], ag[2], ag[3]));
+    }
+  }
+}
+
+// HYBRID: COMPACT until the history is full (kcap = 1024 entries), then the dense matrix.  A problem
+// still running at iteration kcap + 1 folds its history into H once,
+//   H_ij = gamma0 delta_ij + sum_e [ s_ei (c_e rho_e s_ej - rho_e w_ej) - w_ei (rho_e s_ej) ]
+// (the rank-2 terms U_e the history stands for, compact_products), and continues with dense_sweep.  The
+// iteration cap alone never pays for the dense matrix: with the reference's stopping rules problems stop
+// long before 1025 iterations, in the compact phase.  Same mapping as dense_sweep (lane = float4 column
+// group, the wave's share of the groups), so every thread later reads back only what it wrote here;
+// kFoldRows rows per pass in registers, every history entry streamed once per pass.  Entries e < lcap
+// are the LDS-resident ones (LH: S row then W row).  The fold is a sum in entry order, not the
+// reference's sequence of rank-2 updates: the same matrix up to rounding, as COMPACT itself.
+constexpr int kHybrid = 2;  // kernel MODE (internal; callers ask for DAVA_HESSIAN_COMPACT)
+constexpr int kFoldRows = 8;
+template <int NW>
+__device__ void fold_history(int P, int Pv, int Pld, int nh, const float* __restrict__ S, const float* __restrict__ W,
+                             const float* LH, int lcap, const float* hrho, const float* hc, float gamma0,
+                             float* __restrict__ H) {
+  constexpr int R = kFoldRows;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wave = threadIdx.x / kWave;
+  const int G = (P + 3) / 4;
+  const int Gw = (G + NW - 1) / NW;
+  const int g_end = min(G, (wave + 1) * Gw);
+  for (int gb = wave * Gw; gb < g_end; gb += kWave) {
+    const int grp = gb + lane;
+    const bool act = grp < g_end;
+    const int j0 = grp * 4;
+    for (int i0 = 0; i0 < P; i0 += R) {
+      float h[R][4];
+#pragma unroll
+      for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) h[r][q] = i0 + r == j0 + q ? gamma0 : 0.f;
+      for (int e = 0; e < nh; ++e) {
+        const float* sr = e < lcap ? LH + (size_t)2 * e * Pv : S + (size_t)e * Pv;
+        const float* wr = e < lcap ? sr + Pv : W + (size_t)e * Pv;
+        const float rho = hrho[e], crho = hc[e] * rho;
+        float u[4] = {0, 0, 0, 0}, v[4] = {0, 0, 0, 0};
+        if (act) {
+          const float4 s4 = ld4(sr + j0), w4 = ld4(wr + j0);
+          const float sj[4] = {s4.x, s4.y, s4.z, s4.w}, wj[4] = {w4.x, w4.y, w4.z, w4.w};
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            u[q] = crho * sj[q] - rho * wj[q];
+            v[q] = rho * sj[q];
+          }
+        }
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const int i = min(i0 + r, P - 1);  // (rows past P are computed and dropped)
+          const float si = sr[i], wi = wr[i];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) h[r][q] += si * u[q] - wi * v[q];
+        }
+      }
+      if (act)
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+          if (i0 + r < P) {
+            f4v o;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) o[q] = j0 + q < P ? h[r][q] : 0.f;
+            h_store(H + (size_t)(i0 + r) * Pld + j0, o);
+          }
     }
   }
 }
@@ -977,8 +1045,9 @@ __global__ __launch_bounds__(kWave * NW, kSolveWavesPerEU) void bfgs_ba_solve_ke
       b = queued_problem;
       if (b >= a.B) break;
     }
-    const int lcap = MODE == DAVA_HESSIAN_COMPACT && !GV ? a.lcap : 0;
-    const LdsCarve cv = carve_lds(M, N, Pv, MODE == DAVA_HESSIAN_COMPACT ? a.kcap : 0, GV, lcap, XL, NW);
+    constexpr bool kHistory = MODE != DAVA_HESSIAN_DENSE;  // COMPACT, or HYBRID's compact phase
+    const int lcap = kHistory && !GV ? a.lcap : 0;
+    const LdsCarve cv = carve_lds(M, N, Pv, kHistory ? a.kcap : 0, GV, lcap, XL, NW);
     float* LH = lds + cv.hist;  // LDS-resident history entries 0 .. lcap-1
     float* vb0 = GV ? a.vecs + (size_t)b * kVectors * Pv : lds;
     float* x = (GV && !XL ? vb0 : lds) + cv.x;
@@ -1025,7 +1094,7 @@ __global__ __launch_bounds__(kWave * NW, kSolveWavesPerEU) void bfgs_ba_solve_ke
     }
     __syncthreads();
 
-    float* H = nullptr;   // DENSE: this problem's P x Pld inverse Hessian
+    float* H = nullptr;   // DENSE (and HYBRID's dense phase): this problem's P x Pld inverse Hessian
     float* SH = nullptr;  // COMPACT: history rows S[kcap][Pv], W[kcap][Pv]
     float* WH = nullptr;
     if (MODE == DAVA_HESSIAN_DENSE) {
@@ -1033,6 +1102,7 @@ __global__ __launch_bounds__(kWave * NW, kSolveWavesPerEU) void bfgs_ba_solve_ke
     } else if (a.hess) {
       SH = a.hess + (size_t)b * 2 * a.kcap * Pv;
       WH = SH + (size_t)a.kcap * Pv;
+      if (MODE == kHybrid) H = a.hess_dense + (size_t)b * P * a.Pld;
     }
     int buf = 0;
     bool materialized = false;
@@ -1119,6 +1189,18 @@ __global__ __launch_bounds__(kWave * NW, kSolveWavesPerEU) void bfgs_ba_solve_ke
           if constexpr (MODE == DAVA_HESSIAN_DENSE) {
             dense_sweep<NW>(L, a.Pld, H, materialized, gamma0, s_pend, hy_pend, pend_rho, pend_c, g, gp, hy_new, hg);
             materialized = true;
+          } else if (MODE == kHybrid && k - 1 >= a.kcap) {
+            // the history is full: fold it into H (once), then sweep H as DENSE does.  The fold is
+            // H' itself, so this first sweep applies no pending update (zero rows, rho 0: exact).
+            if (!materialized) {
+              for (int i = tid; i < Pv; i += BLOCK) s_pend[i] = hy_pend[i] = 0.f;
+              fold_history<NW>(P, Pv, a.Pld, a.kcap, SH, WH, LH, lcap, hrho, hc, gamma0, H);
+              pend_rho = 0.f;
+              pend_c = 1.f;
+              __syncthreads();
+            }
+            dense_sweep<NW>(L, a.Pld, H, true, gamma0, s_pend, hy_pend, pend_rho, pend_c, g, gp, hy_new, hg);
+            materialized = true;
           } else {
             const int G4 = (P + 3) / 4;
             const int GM = (G4 + kWave - 1) / kWave;
@@ -1195,7 +1277,7 @@ __global__ __launch_bounds__(kWave * NW, kSolveWavesPerEU) void bfgs_ba_solve_ke
           d[i] = di;
           dg += di * g[i];
         }
-        if constexpr (MODE == DAVA_HESSIAN_DENSE) {
+        if (MODE == DAVA_HESSIAN_DENSE || (MODE == kHybrid && k - 1 >= a.kcap)) {
           // the new update becomes the pending one; recycle the old buffers
           { float* t = s_pend; s_pend = s_cur; s_cur = t; }
           { float* t = hy_pend; hy_pend = hy_new; hy_new = t; }
@@ -1521,9 +1603,19 @@ static size_t gv_vector_bytes(const DavaScene* s) {
   return (size_t)s->batch * kVectors * (size_t)round_up(s->num_parameters, 4) * sizeof(float);
 }
 
-// history entries the COMPACT mode needs: one per iteration k = 1 .. iterations-1
-static int compact_capacity(const DavaSolverConfig* c) { return c->iterations > 1 ? c->iterations - 1 : 1; }
+// History entries the COMPACT mode keeps: one per iteration k = 1 .. iterations-1, at most
+// kMaxCompactEntries; a longer solve is HYBRID (fold_history: the dense matrix after the history fills).
+// The kDbgCompactSwitch override lowers the capacity (tests: the switch at K = 30 instead of 1025).
 constexpr int kMaxCompactEntries = 1024;
+static int compact_capacity(const DavaSolverConfig* c) {
+  const int need = c->iterations > 1 ? c->iterations - 1 : 1;
+  const long long sw = debug_knob(kDbgCompactSwitch);
+  const int cap = sw >= 1 && sw < kMaxCompactEntries ? (int)sw : kMaxCompactEntries;
+  return min(need, cap);
+}
+static bool hybrid_solve(const DavaSolverConfig* c) {
+  return c->hessian_mode == DAVA_HESSIAN_COMPACT && c->iterations - 1 > compact_capacity(c);
+}
 
 static size_t compact_history_bytes(const DavaScene* s, const DavaSolverConfig* c) {
   return (size_t)s->batch * 2 * (size_t)compact_capacity(c) * (size_t)round_up(s->num_parameters, 4) * sizeof(float);
@@ -1553,10 +1645,11 @@ using namespace dava;
 
 // ---- debug overrides (dava_debug.hpp): set only through the two calls below, never from the environment ----
 namespace dava {
-static long long g_debug_knobs[kDbgKnobs] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};
+static long long g_debug_knobs[kDbgKnobs] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};
 static const char* const kDebugKnobNames[kDbgKnobs] = {
     "FORCE_GV", "GV_NO_XL", "SOLVE_WAVES", "WG_PER_CU", "LDS_HISTORY", "STAGGER", "STAGGER_LEVELS",
-    "NO_PPT", "NO_QUEUE", "ADJ_GV_WAVES", "ADJ_FORCE_GV", "ADJ_LDS_ENTRIES", "ADJ_GD_HBM"};
+    "NO_PPT", "NO_QUEUE", "ADJ_GV_WAVES", "ADJ_FORCE_GV", "ADJ_LDS_ENTRIES", "ADJ_GD_HBM",
+    "COMPACT_SWITCH"};
 long long debug_knob(int k) { return k >= 0 && k < kDbgKnobs ? g_debug_knobs[k] : -1; }
 }  // namespace dava
 
@@ -1581,7 +1674,8 @@ static size_t solve_state_bytes(const DavaScene* scene, const DavaSolverConfig* 
   const int kcap = config->hessian_mode == DAVA_HESSIAN_COMPACT ? compact_capacity(config) : 0;
   const size_t vec = use_gv(scene, kcap) ? gv_vector_bytes(scene) : 0;
   if (config->hessian_mode == DAVA_HESSIAN_DENSE) return vec + dense_hessian_bytes(scene);
-  return vec + compact_history_bytes(scene, config);
+  // HYBRID: the dense matrices follow the histories (SolveArgs::hess_dense)
+  return vec + compact_history_bytes(scene, config) + (hybrid_solve(config) ? dense_hessian_bytes(scene) : 0);
 }
 
 extern "C" size_t dava_ba_solve_workspace_bytes(const DavaScene* scene, const DavaSolverConfig* config) {
@@ -1604,7 +1698,7 @@ extern "C" int dava_ba_solve_plan(const DavaScene* scene, const DavaSolverConfig
   plan->workgroup_threads = kWave * nw;
   plan->lds_bytes = lds_bytes_for(scene, kcap, gv, lcap, use_xl(scene, kcap, gv), nw);
   plan->lds_history_entries = lcap;
-  return plan->lds_bytes > kMaxLds || kcap > kMaxCompactEntries ? DAVA_ERR_UNSUPPORTED : DAVA_OK;
+  return plan->lds_bytes > kMaxLds ? DAVA_ERR_UNSUPPORTED : DAVA_OK;
 }
 
 constexpr int kStaggerCycles = 20000;  // ~8 us at the shader clock; one C2 iteration is ~47 us
@@ -1686,7 +1780,7 @@ constexpr int kTapeMaxParameters = 14336;
 static bool tape_supported(const DavaScene* scene, const DavaSolverConfig* config) {
   if (config->hessian_mode != DAVA_HESSIAN_COMPACT || config->iterations < 1) return false;
   const int kcap = compact_capacity(config);
-  if (kcap > kMaxCompactEntries || scene->num_parameters > kTapeMaxParameters) return false;
+  if (hybrid_solve(config) || scene->num_parameters > kTapeMaxParameters) return false;
   const bool gv = use_gv(scene, kcap);
   return !gv || wide_history_pass(round_up(scene->num_parameters, 4), kcap, true);
 }
@@ -1709,7 +1803,7 @@ static int solve_impl(const DavaScene* scene, const DavaSolverConfig* config, co
   if (scene->batch == 0) return DAVA_OK;
   if (!x0 || !x_out) return DAVA_ERR_INVALID_ARGUMENT;
   const int kcap = mode == DAVA_HESSIAN_COMPACT ? compact_capacity(config) : 0;
-  if (kcap > kMaxCompactEntries) return DAVA_ERR_UNSUPPORTED;
+  const bool hybrid = hybrid_solve(config);
   const bool gv = use_gv(scene, kcap);
   const bool xl = use_xl(scene, kcap, gv);
   const int nw = solve_waves_for(scene, gv, mode);
@@ -1738,6 +1832,7 @@ static int solve_impl(const DavaScene* scene, const DavaSolverConfig* config, co
   a.status = status_out;
   a.vecs = gv ? static_cast<float*>(workspace) : nullptr;
   a.hess = workspace ? reinterpret_cast<float*>(static_cast<char*>(workspace) + vec) : nullptr;
+  a.hess_dense = hybrid && a.hess ? a.hess + compact_history_bytes(scene, config) / sizeof(float) : nullptr;
   a.c1 = config->sufficient_decrease;
   a.c2 = config->curvature;
   a.thr = config->error_threshold;
@@ -1789,6 +1884,10 @@ static int solve_impl(const DavaScene* scene, const DavaSolverConfig* config, co
     if (xl) launch_solve<DAVA_HESSIAN_DENSE, true, true>(a, scene->batch, lds, s, scene->residual, nw);
     else if (gv) launch_solve<DAVA_HESSIAN_DENSE, true>(a, scene->batch, lds, s, scene->residual, nw);
     else launch_solve<DAVA_HESSIAN_DENSE, false>(a, scene->batch, lds, s, scene->residual, nw);
+  } else if (hybrid) {
+    if (xl) launch_solve<kHybrid, true, true>(a, scene->batch, lds, s, scene->residual, nw);
+    else if (gv) launch_solve<kHybrid, true>(a, scene->batch, lds, s, scene->residual, nw);
+    else launch_solve<kHybrid, false>(a, scene->batch, lds, s, scene->residual, nw);
   } else {
     if (xl) launch_solve<DAVA_HESSIAN_COMPACT, true, true>(a, scene->batch, lds, s, scene->residual, nw);
     else if (gv) launch_solve<DAVA_HESSIAN_COMPACT, true>(a, scene->batch, lds, s, scene->residual, nw);

@@ -23,6 +23,7 @@ enum DebugKnob : int {
   kDbgAdjForceGV,     // 1: global-vector-mode adjoint even where the LDS image fits
   kDbgAdjLdsEntries,  // >= 0: caps the adjoint's on-chip history entries
   kDbgAdjGdHbm,       // 1: the GV adjoint's dual gradient vector in HBM instead of LDS
+  kDbgCompactSwitch,  // >= 1: COMPACT history capacity before the dense fold (default 1024; tests)
   kDbgKnobs
 };
 

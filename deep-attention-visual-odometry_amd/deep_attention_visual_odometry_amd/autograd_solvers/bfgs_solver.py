@@ -226,19 +226,20 @@ class BFGSSolver(Module):
         fraction of the dense bytes -- measured 642.6k vs 77.6k problems/s at C2 and 213.7k vs 9.3k
         at C3 (profiles/r03_defaults_c2_c3.jsonl).  Even a batch that ran every problem to
         K = 1000 would move K Pv / (2 P^2) x the dense bytes (1.27x at C2, 2.5x at C1), streamed
-        at a higher fraction of the HBM peak than the dense sweep."""
+        at a higher fraction of the HBM peak than the dense sweep.
+        Past 1025 iterations compact keeps its first 1024 updates as history and a problem still
+        running at iteration 1025 folds them into the dense matrix and continues dense (the kernel's
+        HYBRID form, csrc/bfgs_solve.hip fold_history): its workspace is the history plus the dense
+        matrices, so 'auto' takes it while that fits and the dense mode otherwise."""
         if self.hessian_mode == "dense":
             return _native.DAVA_HESSIAN_DENSE
-        entries = max(num_iterations - 1, 1)
-        fits = entries <= self.MAX_COMPACT_ENTRIES
         if self.hessian_mode == "compact":
-            if not fits:
-                raise ValueError(f"compact mode supports at most {self.MAX_COMPACT_ENTRIES + 1} iterations")
             return _native.DAVA_HESSIAN_COMPACT
-        if not fits:
-            return _native.DAVA_HESSIAN_DENSE
+        entries = min(max(num_iterations - 1, 1), self.MAX_COMPACT_ENTRIES)
         pv = (p + 3) // 4 * 4
         compact_bytes = batch * 2 * entries * pv * 4
+        if num_iterations - 1 > self.MAX_COMPACT_ENTRIES:
+            compact_bytes += batch * p * ((p + 31) // 32 * 32) * 4
         if compact_bytes > 0.9 * _free_device_bytes(device):  # e.g. B = 65536, K = 1000: 416 GB of history
             return _native.DAVA_HESSIAN_DENSE
         return _native.DAVA_HESSIAN_COMPACT

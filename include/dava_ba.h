@@ -48,7 +48,9 @@ enum DavaStatus {
 /* Representation of the inverse Hessian inside the fused solver. */
 enum DavaHessianMode {
   DAVA_HESSIAN_DENSE = 0,  /* dense P x P fp32 per problem in HBM (the reference's data structure) */
-  DAVA_HESSIAN_COMPACT = 1 /* exact rank-2 update history (s_j, H_{j-1} y_j): same math, O(kP) bytes */
+  DAVA_HESSIAN_COMPACT = 1 /* exact rank-2 update history (s_j, H_{j-1} y_j): same math, O(kP) bytes;
+                            * past 1024 updates (iterations > 1025) a problem that is still running
+                            * folds its history into the dense matrix once and continues DENSE */
 };
 
 /* Why a problem stopped (bfgs_solver.py:143-145, :203-207). */
@@ -375,8 +377,8 @@ int dava_l1_camera_vjp_f64(int64_t batch, int32_t estimates, int32_t views, int3
  * The library makes its launch choices itself (LDS or global-vector mode, waves per workgroup,
  * on-chip history entries, work queue, ...) and reads NOTHING from the environment.  Tests and A/B
  * measurements override a choice by name (FORCE_GV, GV_NO_XL, SOLVE_WAVES, WG_PER_CU, LDS_HISTORY,
- * STAGGER, STAGGER_LEVELS, NO_PPT, NO_QUEUE, ADJ_GV_WAVES, ADJ_FORCE_GV, ADJ_LDS_ENTRIES, ADJ_GD_HBM;
- * csrc/dava_debug.hpp); value < 0 restores the library's choice.  Process-wide, not thread-safe,
+ * STAGGER, STAGGER_LEVELS, NO_PPT, NO_QUEUE, ADJ_GV_WAVES, ADJ_FORCE_GV, ADJ_LDS_ENTRIES, ADJ_GD_HBM,
+ * COMPACT_SWITCH; csrc/dava_debug.hpp); value < 0 restores the library's choice.  Process-wide, not thread-safe,
  * host-only.  DAVA_ERR_INVALID_ARGUMENT for an unknown name.                                     */
 int dava_debug_set_override(const char* name, int64_t value);
 void dava_debug_clear_overrides(void);

@@ -83,6 +83,32 @@ def test_workspace_size_dense(lib):
     assert native_ops.solve_workspace_bytes(8192, 4, 256, True) == 8192 * p * ((p + 31) // 32 * 32) * 4 + 256
 
 
+def test_workspace_size_compact_and_hybrid(lib, overrides):
+    """COMPACT keeps one history entry per update up to 1024 (2 rows of Pv floats each); past 1025
+    iterations it is HYBRID: the 1024-entry history plus the dense matrices it folds into.  The
+    COMPACT_SWITCH override lowers the capacity (the GPU tests' switch at K = 30); a hybrid solve has
+    no tape (the adjoint reads the history of every step)."""
+    from deep_attention_visual_odometry_amd import native_ops
+
+    b, m, n = 64, 4, 256
+    p = 3 + 3 * n + 6 * (m - 1) + 5
+    pv, pld = (p + 3) // 4 * 4, (p + 31) // 32 * 32
+    dense = b * p * pld * 4
+    ws = lambda k: native_ops.solve_workspace_bytes(b, m, n, True, 1, k)  # noqa: E731
+    assert ws(100) == b * 2 * 99 * pv * 4 + 256
+    assert ws(1025) == b * 2 * 1024 * pv * 4 + 256
+    assert ws(1026) == ws(5000) == b * 2 * 1024 * pv * 4 + dense + 256
+    assert native_ops.solve_plan(b, m, n, True, 1, 5000)["workgroup_threads"] == 256  # no longer refused
+    sc = native_ops.scene_struct(None, None, m, n, True, b)
+    tape = lambda k: lib.dava_ba_solve_tape_bytes(  # noqa: E731
+        sc, native_ops.solver_config(1e-4, 0.9, -1.0, k, -1.0, 1000, True, 1))
+    assert tape(30) > 0 and tape(1025) > 0 and tape(1026) == 0
+    overrides("COMPACT_SWITCH", 8)
+    assert ws(30) == b * 2 * 8 * pv * 4 + dense + 256
+    assert ws(9) == b * 2 * 8 * pv * 4 + 256
+    assert tape(30) == 0 and tape(9) > 0
+
+
 def test_solve_plan(lib, overrides):
     """Host-only plan query: C3 keeps its oldest history entries in LDS within two workgroups
     per CU; C5 (P = 12381) runs the O(P) state from HBM in 512-thread workgroups."""
