@@ -83,6 +83,10 @@ def parse(argv=None):
     p.add_argument("--no-live-counters", action="store_true",
                    help="skip the rocprofv3 FETCH_SIZE / WRITE_SIZE child passes and the history-stream ceiling run "
                         "that follow the timed region at N = 1 (roofline.traffic then comes from the committed summary)")
+    p.add_argument("--sustain-seconds", type=float, default=10.0,
+                   help="after the timed region, keep solving the same batch for about this long (same step, no "
+                        "collective) and report the sustained rate beside the timed one (clocks and power at "
+                        "steady state; a phase long enough for a GPU-busy sampler to see).  0 = skip")
     p.add_argument("--launch-test", action="store_true",
                    help="multi-rank LAUNCH plumbing check on CPU (gloo, identity stub instead of the solve); "
                         "prints a line marked as a launch test, never a measurement")
@@ -405,6 +409,9 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
     ranks = per_rank_phases(kernel_ms, gather_ms, world, dev) if world > 1 else None
+    sustained = None
+    if args.sustain_seconds > 0 and not launch_test and not args.differentiate:
+        sustained = sustain(args, solve, sync, elapsed / args.steps, world, b, dev)
 
     if gathered is not None:  # diagnostics over the whole global batch
         x_all, st = gathered[0].cpu(), gathered[1].cpu()
@@ -438,6 +445,9 @@ def main():
         else:
             line = measurement_line(args, base, world, b, p, mn, distortion, ray, plan, kernel_ms, st, finite, x0_cpu,
                                     obs_cpu, vis_cpu, x)
+            if sustained is not None:
+                sustained["ratio_to_value"] = round(sustained["value"] / value, 4)
+                line["sustained"] = sustained
             if world > 1:
                 line["per_rank"] = ranks
                 line["spot_check"] = spot_check(args, x0_cpu, obs_cpu, vis_cpu, x_all, distortion, ray)
@@ -445,6 +455,30 @@ def main():
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def sustain(args, solve, sync, step_s, world, b, dev):
+    """The same solve, back to back for about --sustain-seconds after the timed region (no collective: each
+    rank's own slab), bracketed like the timed region (sync + barrier, max over ranks).  The step count is
+    fixed from the timed region's step time, so every rank runs the same number."""
+    n = max(1, int(round(args.sustain_seconds / max(step_s, 1e-6))))
+    sync()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(n):
+        solve()
+    sync()
+    if world > 1:
+        dist.barrier()
+    t = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([t], device=dev, dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        t = tt.item()
+    return {"seconds": round(t, 3), "steps": n, "value": round(world * b * n / t, 2), "unit": "problems/s",
+            "note": "the timed step repeated back to back after the timed region (rank-local solves, no gather); "
+                    "steady-state clocks and power, not the headline value"}
 
 
 def _config_argv(args):
@@ -476,7 +510,7 @@ def live_traffic(args, kernel="bfgs_ba_solve_kernel"):
             out = os.path.join(tmp, counter)
             cmd = [prof, "--pmc", counter, "-d", out, "-o", "p", "--output-format", "csv", "--",
                    sys.executable, os.path.abspath(__file__), "--steps", "1", "--warmup", "0", "--cpu-sample", "0",
-                   "--no-live-counters"] + _config_argv(args)
+                   "--no-live-counters", "--sustain-seconds", "0"] + _config_argv(args)
             env = dict(os.environ, TMPDIR="/tmp")
             try:
                 r = subprocess.run(cmd, cwd="/tmp", env=env, capture_output=True, text=True, timeout=180)

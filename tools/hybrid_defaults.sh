@@ -7,7 +7,7 @@ cd "${GRAFT_REPO_ROOT:-$(pwd)}"
 mkdir -p gpurun_out
 out=gpurun_out/hybrid_defaults.jsonl
 : > "$out"
-common="--iterations ${ITERS:-2000} --error-threshold 1e-4 --minimum-step 1e-8 --cpu-sample 0 --parity-envelope 0 --no-live-counters --steps 3 --warmup 1"
+common="--iterations ${ITERS:-2000} --error-threshold 1e-4 --minimum-step 1e-8 --cpu-sample 0 --parity-envelope 0 --no-live-counters --sustain-seconds 0 --steps 3 --warmup 1"
 for cfg in "C2:--views 2 --points 128 --no-distortion" "C3:"; do
   tag=${cfg%%:*}; args=${cfg#*:}
   for mode in compact dense; do

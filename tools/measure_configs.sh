@@ -7,7 +7,7 @@ OUT=$R/gpurun_out/configs.jsonl
 : > "$OUT"
 run() {
   local tag=$1; shift
-  if timeout -k 10 600 python3 "$R/bench.py" --cpu-sample 0 "$@" > "$R/gpurun_out/cfg_$tag.log" 2>&1; then
+  if timeout -k 10 600 python3 "$R/bench.py" --cpu-sample 0 --sustain-seconds 0 "$@" > "$R/gpurun_out/cfg_$tag.log" 2>&1; then
     echo "{\"tag\": \"$tag\", \"line\": $(tail -1 "$R/gpurun_out/cfg_$tag.log")}" >> "$OUT"
   else
     echo "config $tag failed"; tail -5 "$R/gpurun_out/cfg_$tag.log"; return 1

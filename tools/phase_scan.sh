@@ -8,7 +8,7 @@ LIB=$R/deep-attention-visual-odometry_amd/build/var_phase/libdava_ba.so
 run() {
   echo "== $1"
   shift
-  env DAVA_DEBUG_OVERRIDES=1 DAVA_LIB=$LIB timeout -k 10 300 python3 "$R/bench.py" --cpu-sample 0 --no-live-counters --steps 1 --warmup 0 "$@" 2>&1 \
+  env DAVA_DEBUG_OVERRIDES=1 DAVA_LIB=$LIB timeout -k 10 300 python3 "$R/bench.py" --cpu-sample 0 --no-live-counters --sustain-seconds 0 --steps 1 --warmup 0 "$@" 2>&1 \
     | grep -E "dava (phase|objective) cycles" || return 1
 }
 run C2_b64 --batch 64 --views 2 --points 128 --no-distortion &&

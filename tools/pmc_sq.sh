@@ -22,7 +22,7 @@ for set in "$A" "$B" "$C"; do
       python3 "$R/$PROG" "$@" > "$OUT/p$i.log" 2>&1 || { echo "pass $i failed"; tail -5 "$OUT/p$i.log"; exit 1; }
   else
     timeout -s KILL 120 rocprofv3 --pmc $set -d "$OUT/p$i" -o p$i --output-format csv -- \
-      python3 "$R/bench.py" --cpu-sample 0 --no-live-counters --steps 1 --warmup 0 "$@" > "$OUT/p$i.log" 2>&1 || { echo "pass $i failed"; tail -5 "$OUT/p$i.log"; exit 1; }
+      python3 "$R/bench.py" --cpu-sample 0 --no-live-counters --sustain-seconds 0 --steps 1 --warmup 0 "$@" > "$OUT/p$i.log" 2>&1 || { echo "pass $i failed"; tail -5 "$OUT/p$i.log"; exit 1; }
   fi
 done
 python3 - "$OUT" "$KERNEL" <<'PY'

@@ -12,9 +12,9 @@ OUT=$R/gpurun_out/prof_$TAG
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/kt" -o kt --output-format csv -- \
-  python3 "$R/bench.py" --cpu-sample 0 --no-live-counters "$@" > "$OUT/kt_bench.log" 2>&1
+  python3 "$R/bench.py" --cpu-sample 0 --no-live-counters --sustain-seconds 0 "$@" > "$OUT/kt_bench.log" 2>&1
 timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/fetch" -o fetch --output-format csv -- \
-  python3 "$R/bench.py" --cpu-sample 0 --no-live-counters --steps 1 --warmup 0 "$@" > "$OUT/fetch_bench.log" 2>&1
+  python3 "$R/bench.py" --cpu-sample 0 --no-live-counters --sustain-seconds 0 --steps 1 --warmup 0 "$@" > "$OUT/fetch_bench.log" 2>&1
 timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE -d "$OUT/write" -o write --output-format csv -- \
-  python3 "$R/bench.py" --cpu-sample 0 --no-live-counters --steps 1 --warmup 0 "$@" > "$OUT/write_bench.log" 2>&1
+  python3 "$R/bench.py" --cpu-sample 0 --no-live-counters --sustain-seconds 0 --steps 1 --warmup 0 "$@" > "$OUT/write_bench.log" 2>&1
 echo "profile $TAG done"
