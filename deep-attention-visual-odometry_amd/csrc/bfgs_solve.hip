@@ -201,7 +201,7 @@ __device__ __forceinline__ float rank2(float h, float sri, float sj, float c, fl
 // access is a contiguous row piece of up to 1 KiB.  Lane = column means the
 // column sums need no cross-lane reduction.  U rows are loaded before any is
 // consumed to keep U KiB per wave in flight.
-template <int NW>
+template <int NW, bool PIPE>
 __device__ __forceinline__ void dense_sweep(const Layout& L, int Pld, float* __restrict__ H, bool materialized, float gamma0,
                             const float* ps, const float* phy, float prho, float pc, const float* g,
                             const float* gp, float* hy_out, float* hg_out) {
@@ -244,7 +244,72 @@ __device__ __forceinline__ void dense_sweep(const Layout& L, int Pld, float* __r
       return h;
     };
     int i = 0;
-    if (materialized) {
+    if (PIPE && materialized) {
+      // Global-vector mode (one problem per CU, rows of thousands of groups): software-pipelined,
+      // two batches of U rows in flight per wave, through buffer loads / stores (a lane past the
+      // wave's groups gets an offset past the descriptor's range: its load returns 0 and its store
+      // is dropped, no branch).  Without branches around the memory operations the compiler waits
+      // vmcnt(8..11) before a row instead of the vmcnt(0) the predicated loads force (a full round
+      // trip plus the previous batch's stores per batch).  The batches ahead are clamped to row P - 1
+      // (a few redundant loads at the end, never consumed).  Same arithmetic, same order: bitwise.
+      // C5 dense +4.9%; the LDS-mode kernels keep the predicated loop below: there (C3, two problems
+      // per CU) the same change measured -2.8%, one batch ahead -0.4%, and 8 or 16 rows per batch
+      // -0.4 / -2.7% (profiles/r05_ab_dense_sweep_pipe.log, r01_ab_sweep_variants.log).
+      const auto rs = make_rsrc(H, P * Pld * (int)sizeof(float));
+      const unsigned rowb = (unsigned)Pld * 4u;
+      const unsigned base = act ? (unsigned)j0 * 4u : 0x80000000u;
+      auto ldrow = [&](int r) {
+        return __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(base + (unsigned)r * rowb), 0, 0));
+      };
+      auto strow = [&](int r, f4v h) {
+        typedef unsigned u4v __attribute__((ext_vector_type(4)));
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, h), rs, (int)(base + (unsigned)r * rowb), 0, 0);
+      };
+      auto update = [&](int r, f4v h, float gi, float gpi, float psi, float phyi) {
+        const float yi = gi - gpi;
+        const float sri = __fmul_rn(psi, prho), hyi = phyi;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          h[k] = rank2(h[k], sri, sj[k], pc, hj[k], hyi, srj[k]);
+          ay[k] += h[k] * yi;
+          ag[k] += h[k] * gi;
+        }
+        strow(r, h);
+      };
+      static_assert(U == 4, "the row scalars are read as float4");
+      auto consume = [&](int r0, const f4v* h) {
+        const float4 g4 = ld4(g + r0), gp4 = ld4(gp + r0), ps4 = ld4(ps + r0), phy4 = ld4(phy + r0);
+        update(r0, h[0], g4.x, gp4.x, ps4.x, phy4.x);
+        update(r0 + 1, h[1], g4.y, gp4.y, ps4.y, phy4.y);
+        update(r0 + 2, h[2], g4.z, gp4.z, ps4.z, phy4.z);
+        update(r0 + 3, h[3], g4.w, gp4.w, ps4.w, phy4.w);
+      };
+      auto tail = [&](int r0, const f4v* h) {
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+          if (r0 + u < P) update(r0 + u, h[u], g[r0 + u], gp[r0 + u], ps[r0 + u], phy[r0 + u]);
+      };
+      // two batches in flight, rotated without register copies (a copy would wait for the loads)
+      f4v A[U], Bq[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) A[u] = ldrow(min(u, P - 1));
+#pragma unroll
+      for (int u = 0; u < U; ++u) Bq[u] = ldrow(min(U + u, P - 1));
+      for (; i + 2 * U <= P; i += 2 * U) {
+        consume(i, A);
+#pragma unroll
+        for (int u = 0; u < U; ++u) A[u] = ldrow(min(i + 2 * U + u, P - 1));
+        consume(i + U, Bq);
+#pragma unroll
+        for (int u = 0; u < U; ++u) Bq[u] = ldrow(min(i + 3 * U + u, P - 1));
+      }
+      if (i + U <= P) {
+        consume(i, A);
+        tail(i + U, Bq);
+      } else {
+        tail(i, A);
+      }
+    } else if (materialized) {
       for (; i + U <= P; i += U) {
         f4v h[U];
 #pragma unroll
@@ -1187,7 +1252,7 @@ __global__ __launch_bounds__(kWave * NW, kSolveWavesPerEU) void bfgs_ba_solve_ke
           // (no barrier needed: each thread reads back only its own hy_new / hg below)
         } else {
           if constexpr (MODE == DAVA_HESSIAN_DENSE) {
-            dense_sweep<NW>(L, a.Pld, H, materialized, gamma0, s_pend, hy_pend, pend_rho, pend_c, g, gp, hy_new, hg);
+            dense_sweep<NW, GV>(L, a.Pld, H, materialized, gamma0, s_pend, hy_pend, pend_rho, pend_c, g, gp, hy_new, hg);
             materialized = true;
           } else if (MODE == kHybrid && k - 1 >= a.kcap) {
             // the history is full: fold it into H (once), then sweep H as DENSE does.  The fold is
@@ -1199,7 +1264,7 @@ __global__ __launch_bounds__(kWave * NW, kSolveWavesPerEU) void bfgs_ba_solve_ke
               pend_c = 1.f;
               __syncthreads();
             }
-            dense_sweep<NW>(L, a.Pld, H, true, gamma0, s_pend, hy_pend, pend_rho, pend_c, g, gp, hy_new, hg);
+            dense_sweep<NW, GV>(L, a.Pld, H, true, gamma0, s_pend, hy_pend, pend_rho, pend_c, g, gp, hy_new, hg);
             materialized = true;
           } else {
             const int G4 = (P + 3) / 4;

@@ -2,7 +2,7 @@
 each in a fresh subprocess, compared problem by problem: bitwise-equal rows, rows that differ, and
 rows that are non-finite in either.  A change meant to touch only overflowing problems (e.g. the
 non-finite trial-slope rule) must leave every finite row bitwise unchanged.
-usage: python tools/lib_compare.py LIB_A LIB_B [--seed 7] [--batch 8192] [--k 100]
+usage: python tools/lib_compare.py LIB_A LIB_B [--seed 7] [--batch 8192] [--k 100] [--mode 0|1]
 """
 import argparse
 import os
@@ -20,7 +20,7 @@ s = make_scenes(%(batch)d, %(m)d, %(n)d, distortion=%(dist)r, seed=%(seed)d)
 dev = torch.device("cuda", 0)
 x0, obs, vis = (torch.tensor(a, device=dev) for a in (s.initial, s.observations, s.visibility))
 x, _, st = native_ops.ba_solve(x0, obs, vis, %(m)d, %(n)d, %(dist)r, iterations=%(k)d, error_threshold=-1.0,
-                               minimum_step=-1.0, hessian_mode=1, want_status=True)
+                               minimum_step=-1.0, hessian_mode=%(mode)d, want_status=True)
 np.savez(%(out)r, x=x.cpu().numpy(), st=st.cpu().numpy())
 """
 
@@ -35,6 +35,7 @@ def main():
     ap.add_argument("--points", type=int, default=256)
     ap.add_argument("--no-distortion", action="store_true")
     ap.add_argument("--k", type=int, default=100)
+    ap.add_argument("--mode", type=int, default=1, help="0 = DENSE, 1 = COMPACT")
     args = ap.parse_args()
     import numpy as np
 
@@ -43,7 +44,7 @@ def main():
     for tag, lib in (("a", args.lib_a), ("b", args.lib_b)):
         out = os.path.join(tmp, tag + ".npz")
         code = CHILD % dict(repo=REPO, batch=args.batch, m=args.views, n=args.points, dist=not args.no_distortion,
-                            seed=args.seed, k=args.k, out=out)
+                            seed=args.seed, k=args.k, out=out, mode=args.mode)
         subprocess.run([sys.executable, "-c", code], env=dict(os.environ, DAVA_DEBUG_OVERRIDES="1", DAVA_LIB=os.path.abspath(lib)),
                        check=True, timeout=300)
         res[tag] = np.load(out)
