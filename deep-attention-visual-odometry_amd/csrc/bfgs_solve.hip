@@ -579,7 +579,10 @@ __device__ __forceinline__ void compact_products_wide(int P, int Pv, int nh, con
 // free registers for two entries per reduction -- bitwise equal, but the per-entry LDS re-reads and
 // the spills cost 14% with one entry and 19% with two.  Forming only H'g from the history and
 // H'y = H'g + d_prev: two entries per reduction, +0.5..0.9% at C5 but a different rounding that moved
-// a C2 problem 2.1e-5 from the oracle, profiles/r03_ab_hy_from_d.log.)
+// a C2 problem 2.1e-5 from the oracle, profiles/r03_ab_hy_from_d.log.  r05, in the microbenchmark
+// tools/micro/wide_pass_stream.hip: each wave owning a contiguous segment of every row instead of the
+// strided groups t, t + BLOCK, ... -- 4.68 vs 4.76 us per entry staged, 4.74 vs 4.71 in registers at
+// B = 256, another rounding; not adopted, profiles/r05_micro_wide_pass_ownership.log.)
 template <int GT, int NW, bool STAGED = false, int ROWSLOTS = 2>
 __device__ __forceinline__ float wide_direction(int P, int Pv, int nh, const float* __restrict__ S,
                                                 const float* __restrict__ W, float* hrho, float* hc, float gamma0,
