@@ -84,3 +84,24 @@ def test_hybrid_with_stopping_rules_is_the_compact_solve(device):
     stopped = s_c[:, 1] != 0
     assert stopped.float().mean() >= 0.9, s_c
     assert torch.equal(x_c[stopped], x_h[stopped]) and torch.equal(s_c[stopped], s_h[stopped])
+
+
+@pytest.mark.parametrize("knobs", [{}, {"FORCE_GV": 1}])
+def test_hybrid_switch_ray_angle_matches_oracle(device, knobs, overrides):
+    """The hybrid kernel with the ray-angle residual (CalibrationNetwork's error, its own template
+    instantiations): capacity 8 at K = 10, LDS mode and global-vector mode, against the oracle's
+    RayAngleClosure at the fixed-K bar used for that residual at this shape
+    (test_ray_angle_fixed_iterations_match_oracle_c3_shape)."""
+    from deep_attention_visual_odometry_amd import make_scenes
+    from test_gpu_solver import _gpu_solve_ray
+
+    s = make_scenes(2, 4, 256, seed=332, drop=0.1, ray_angle=True)
+    x0, obs, vis = torch.tensor(s.initial), torch.tensor(s.observations), torch.tensor(s.visibility)
+    kw = dict(iterations=10, error_threshold=-1.0, minimum_step=-1.0)
+    ref = solver.bfgs_solve(x0, objective.RayAngleClosure(obs, vis, 4, 256), **kw)
+    for name, value in knobs.items():
+        overrides(name, value)
+    overrides("COMPACT_SWITCH", 4)
+    out, status = _gpu_solve_ray(device, x0, obs, vis, 4, 256, hessian_mode="compact", **kw)
+    assert (status[:, 0] == 10).all()
+    assert _rel(out, ref).max() <= TOL, _rel(out, ref)
