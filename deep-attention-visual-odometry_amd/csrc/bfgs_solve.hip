@@ -46,7 +46,10 @@ struct SolveArgs {
   int iters, max_trials, strong, mode;
   int kcap;       // COMPACT: history capacity (entries)
   int lcap;       // COMPACT, LDS mode: entries 0 .. lcap-1 live in LDS instead of HBM
-  float* vecs;    // GV mode: B x kVectors x Pv floats (else unused)
+  float* vecs;    // GV mode: B slices of vstride floats (kVectors x Pv, then rho_j / c_j if scal_slice)
+  int vstride;
+  int scal_slice;  // GV, wide pass: rho_j, c_j in the workspace slice instead of LDS
+  int kcap_lds;    // history entries whose rho_j, c_j (and product coefficients) the LDS image holds
   unsigned long long* phase_cycles;  // DAVA_PHASE_TIMING builds: B x kPhases (else null)
   int* queue;     // work-queue counter (zeroed before the launch), or null: problem = blockIdx.x
   // recording solve (dava_ba_solve_record, dava_tape.hpp): x_k and g_k rows, (alpha, rho, c, gamma)
@@ -97,6 +100,18 @@ constexpr int kWideMaxGroups = 7;
 constexpr int kGvEntries = DAVA_GV_ENTRIES;
 __host__ __device__ inline bool wide_history_pass(int Pv, int kcap, bool gv) {
   return gv && kcap > 0 && (Pv / 4 + kWave * solve_waves(gv) - 1) / (kWave * solve_waves(gv)) <= kWideMaxGroups;
+}
+// GV mode, wide pass: where each history entry's rho_j and c_j live.  In LDS (beside the product
+// coefficients, 24 B per entry) while the XL image (x, d and the objective's gradient, 149 KB at C5) still
+// fits beside them; past that (C5: ~320 iterations, e.g. the reference's default cap of 1000) in the
+// problem's workspace slice, after its kVectors vectors (round_up(kcap, 64) floats each), so that the XL
+// image stays: without it the solve ran at 4.80k against 7.22k problems/s at K = 100
+// (profiles/r05_ab_c5_xl.log); at K = 400 the slice form runs 689 against 539 problems/s, and K = 100
+// (LDS, as before) is unchanged (profiles/r05_ab_c5_scalar_slice.log).  The pass reads entry j's pair
+// with one uniform load each, issued at the entry's start and needed only after its block reduction.
+__host__ __device__ inline int gv_scalar_stride(int kcap) { return round_up(kcap, 64); }
+__host__ __device__ inline int gv_slice_floats(int Pv, int kcap, bool scalars_in_slice) {
+  return kVectors * Pv + (scalars_in_slice ? 2 * gv_scalar_stride(kcap) : 0);
 }
 
 // LDS image of one problem.  In global-vector (GV) mode -- large P, where the O(P)
@@ -1069,9 +1084,15 @@ __device__ __forceinline__ void compact_products_fused(int P, int Pv, int nh, co
 // each thread's (<= PPT) points in registers across the view sweep (ba_eval).
 // NW: waves per workgroup -- 8 in GV mode; 4 (default) or 2 in LDS mode (two-wave workgroups put
 // twice as many small problems on a CU at once, DESIGN.md 3.1 Launch).
-template <int MODE, bool GV, int RES, bool XL, int PPT, int NW>
+// SLICE: the GV wide pass's rho_j, c_j in the workspace slice (gv_scalar_stride), a kernel of its own:
+// chosen at run time inside one kernel, the two forms cost both 1-10% to register allocation
+// (profiles/r05_ab_c5_scalar_slice.log).  (The LDS image's scalar capacity stays a run-time argument,
+// kcap_lds: with the constant 0 in the SLICE kernels this compiler rejects the kernel with an illegal
+// V_CMP_NE_U32 on src_shared_base.)
+template <int MODE, bool GV, int RES, bool XL, int PPT, int NW, bool SLICE = false>
 __global__ __launch_bounds__(kWave * NW, kSolveWavesPerEU) void bfgs_ba_solve_kernel(SolveArgs a) {
   static_assert(!XL || GV, "XL is a global-vector-mode variant");
+  static_assert(!SLICE || (GV && MODE != DAVA_HESSIAN_DENSE), "SLICE is a global-vector history variant");
   static_assert(GV ? NW == solve_waves(true) : (NW == 1 || NW == 2 || NW == 4), "LDS mode runs 1-, 2- or 4-wave workgroups");
   constexpr int BLOCK = kWave * NW;
   constexpr bool kTrialDot = GV ? kTrialDotGv : kTrialDotLds;
@@ -1115,9 +1136,10 @@ __global__ __launch_bounds__(kWave * NW, kSolveWavesPerEU) void bfgs_ba_solve_ke
     }
     constexpr bool kHistory = MODE != DAVA_HESSIAN_DENSE;  // COMPACT, or HYBRID's compact phase
     const int lcap = kHistory && !GV ? a.lcap : 0;
-    const LdsCarve cv = carve_lds(M, N, Pv, kHistory ? a.kcap : 0, GV, lcap, XL, NW);
+    constexpr bool gvs = SLICE;  // rho_j, c_j in the workspace slice
+    const LdsCarve cv = carve_lds(M, N, Pv, kHistory ? a.kcap_lds : 0, GV, lcap, XL, NW);
     float* LH = lds + cv.hist;  // LDS-resident history entries 0 .. lcap-1
-    float* vb0 = GV ? a.vecs + (size_t)b * kVectors * Pv : lds;
+    float* vb0 = GV ? a.vecs + (size_t)b * a.vstride : lds;
     float* x = (GV && !XL ? vb0 : lds) + cv.x;
     float* d = (GV && !XL ? vb0 : lds) + cv.d;
     float* ge = lds + cv.ge;  // XL: the objective's gradient output, copied to g / gp after each evaluation
@@ -1132,8 +1154,8 @@ __global__ __launch_bounds__(kWave * NW, kSolveWavesPerEU) void bfgs_ba_solve_ke
     float* g = vb0 + cv.g0;
     float* gp = vb0 + cv.g1;
     float* hcoef = lds + cv.hcoef;
-    float* hrho = lds + cv.hrho;
-    float* hc = lds + cv.hc;
+    float* hrho = gvs ? vb0 + kVectors * Pv : lds + cv.hrho;
+    float* hc = gvs ? hrho + gv_scalar_stride(a.kcap) : lds + cv.hc;
     float* s_cur = vb0 + cv.s0;
     float* s_pend = vb0 + cv.s1;
     float* hy_new = vb0 + cv.hy0;
@@ -1629,9 +1651,26 @@ static size_t dense_hessian_bytes(const DavaScene* s) {
   return (size_t)s->batch * (size_t)P * (size_t)round_up(P, 32) * sizeof(float);
 }
 
+constexpr int kMaxLds = 160 * 1024;
+constexpr int kSliceMinGroups = 6;
+// GV mode, wide pass: rho_j, c_j move to the workspace slice when that keeps the XL image on-chip
+// (see gv_scalar_stride)
+static bool gv_scalars_slice(const DavaScene* s, int kcap) {
+  const int Pv = round_up(s->num_parameters, 4);
+  if (!wide_history_pass(Pv, kcap, true)) return false;
+  // only rows of >= 6 float4 groups per thread have the slice form instantiated (wide_direction SLICE):
+  // narrower rows leave room for the scalars beside their XL image at any cap
+  if ((Pv / 4 + kWave * solve_waves(true) - 1) / (kWave * solve_waves(true)) < kSliceMinGroups) return false;
+  if (debug_knob(kDbgGvScalarSlice) >= 0) return debug_knob(kDbgGvScalarSlice) > 0;  // tests
+  const int M = s->num_views, N = s->num_points, nw = solve_waves(true);
+  return carve_lds(M, N, Pv, kcap, true, 0, true, nw).total_bytes > kMaxLds &&
+         carve_lds(M, N, Pv, 0, true, 0, true, nw).total_bytes <= kMaxLds;
+}
 static int lds_bytes_for(const DavaScene* s, int kcap = 0, bool gv = false, int lcap = 0, bool xl = false,
                          int nw = 0) {
-  return carve_lds(s->num_views, s->num_points, round_up(s->num_parameters, 4), kcap, gv, lcap, xl, nw).total_bytes;
+  const int Pv = round_up(s->num_parameters, 4);
+  const int kl = gv && xl && gv_scalars_slice(s, kcap) ? 0 : kcap;  // (the slice form exists with XL only)
+  return carve_lds(s->num_views, s->num_points, Pv, kl, gv, lcap, xl, nw).total_bytes;
 }
 
 // Waves per LDS-mode workgroup (GV mode: always 8).  The register budget (256 VGPRs) holds two
@@ -1657,7 +1696,6 @@ static int solve_waves_for(const DavaScene* s, bool gv, int mode) {
 // Global-vector mode when the all-in-LDS image would cost more than two workgroups
 // per CU (e.g. C5: P = 12381 -> 446 KB of vectors per problem).
 constexpr int kLdsModeBudget = 72 * 1024;
-constexpr int kMaxLds = 160 * 1024;
 static bool use_gv(const DavaScene* s, int kcap = 0) {
   return debug_flag(kDbgForceGV) || lds_bytes_for(s, kcap, false) > kLdsModeBudget;
 }
@@ -1667,8 +1705,13 @@ static bool use_xl(const DavaScene* s, int kcap, bool gv) {
   if (!gv || debug_flag(kDbgGVNoXL)) return false;
   return lds_bytes_for(s, kcap, true, 0, true) <= kMaxLds;
 }
-static size_t gv_vector_bytes(const DavaScene* s) {
-  return (size_t)s->batch * kVectors * (size_t)round_up(s->num_parameters, 4) * sizeof(float);
+// the launch keeps rho_j, c_j in the workspace slice (bfgs_ba_solve_kernel SLICE)
+static bool gv_slice_used(const DavaScene* s, int kcap) {
+  return use_xl(s, kcap, true) && gv_scalars_slice(s, kcap);
+}
+static size_t gv_vector_bytes(const DavaScene* s, int kcap) {
+  return (size_t)s->batch * (size_t)gv_slice_floats(round_up(s->num_parameters, 4), kcap, gv_slice_used(s, kcap)) *
+         sizeof(float);
 }
 
 // History entries the COMPACT mode keeps: one per iteration k = 1 .. iterations-1, at most
@@ -1713,11 +1756,11 @@ using namespace dava;
 
 // ---- debug overrides (dava_debug.hpp): set only through the two calls below, never from the environment ----
 namespace dava {
-static long long g_debug_knobs[kDbgKnobs] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};
+static long long g_debug_knobs[kDbgKnobs] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};
 static const char* const kDebugKnobNames[kDbgKnobs] = {
     "FORCE_GV", "GV_NO_XL", "SOLVE_WAVES", "WG_PER_CU", "LDS_HISTORY", "STAGGER", "STAGGER_LEVELS",
     "NO_PPT", "NO_QUEUE", "ADJ_GV_WAVES", "ADJ_FORCE_GV", "ADJ_LDS_ENTRIES", "ADJ_GD_HBM",
-    "COMPACT_SWITCH"};
+    "COMPACT_SWITCH", "GV_SCALAR_SLICE"};
 long long debug_knob(int k) { return k >= 0 && k < kDbgKnobs ? g_debug_knobs[k] : -1; }
 }  // namespace dava
 
@@ -1740,7 +1783,7 @@ extern "C" void dava_debug_clear_overrides(void) {
 constexpr size_t kQueueBytes = 256;
 static size_t solve_state_bytes(const DavaScene* scene, const DavaSolverConfig* config) {
   const int kcap = config->hessian_mode == DAVA_HESSIAN_COMPACT ? compact_capacity(config) : 0;
-  const size_t vec = use_gv(scene, kcap) ? gv_vector_bytes(scene) : 0;
+  const size_t vec = use_gv(scene, kcap) ? gv_vector_bytes(scene, kcap) : 0;
   if (config->hessian_mode == DAVA_HESSIAN_DENSE) return vec + dense_hessian_bytes(scene);
   // HYBRID: the dense matrices follow the histories (SolveArgs::hess_dense)
   return vec + compact_history_bytes(scene, config) + (hybrid_solve(config) ? dense_hessian_bytes(scene) : 0);
@@ -1771,9 +1814,9 @@ extern "C" int dava_ba_solve_plan(const DavaScene* scene, const DavaSolverConfig
 
 constexpr int kStaggerCycles = 20000;  // ~8 us at the shader clock; one C2 iteration is ~47 us
 
-template <int MODE, bool GV, int RES, bool XL, int PPT, int NW>
+template <int MODE, bool GV, int RES, bool XL, int PPT, int NW, bool SLICE = false>
 static void launch_solve_ppt(const SolveArgs& a, int B, int lds, hipStream_t s) {
-  const auto kernel = bfgs_ba_solve_kernel<MODE, GV, RES, XL, PPT, NW>;
+  const auto kernel = bfgs_ba_solve_kernel<MODE, GV, RES, XL, PPT, NW, SLICE>;
   constexpr int threads = kWave * NW;
   if (lds > 64 * 1024)
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize, lds);
@@ -1817,27 +1860,29 @@ static void launch_solve_ppt(const SolveArgs& a, int B, int lds, hipStream_t s) 
 template <bool GV, bool XL, int NW>
 constexpr int kRegisterPoints = GV ? 0 : (NW == 1 ? 2 : 1);
 
-template <int MODE, bool GV, int RES, bool XL, int NW>
+template <int MODE, bool GV, int RES, bool XL, int NW, bool SLICE = false>
 static void launch_solve_nw(const SolveArgs& a, int B, int lds, hipStream_t s) {
   constexpr int R = kRegisterPoints<GV, XL, NW>;
-  if (R > 0 && a.L.N <= R * kWave * NW && !debug_flag(kDbgNoPPT))
+  if constexpr (SLICE)  // (GV: no points in registers)
+    launch_solve_ppt<MODE, GV, RES, XL, 0, NW, SLICE>(a, B, lds, s);
+  else if (R > 0 && a.L.N <= R * kWave * NW && !debug_flag(kDbgNoPPT))
     launch_solve_ppt<MODE, GV, RES, XL, R, NW>(a, B, lds, s);
   else
     launch_solve_ppt<MODE, GV, RES, XL, 0, NW>(a, B, lds, s);
 }
 
-template <int MODE, bool GV, int RES, bool XL>
+template <int MODE, bool GV, int RES, bool XL, bool SLICE = false>
 static void launch_solve_res(const SolveArgs& a, int B, int lds, hipStream_t s, int nw) {
-  if constexpr (GV) launch_solve_nw<MODE, GV, RES, XL, solve_waves(true)>(a, B, lds, s);
+  if constexpr (GV) launch_solve_nw<MODE, GV, RES, XL, solve_waves(true), SLICE>(a, B, lds, s);
   else if (nw == 1) launch_solve_nw<MODE, GV, RES, XL, 1>(a, B, lds, s);
   else if (nw == 2) launch_solve_nw<MODE, GV, RES, XL, 2>(a, B, lds, s);
   else launch_solve_nw<MODE, GV, RES, XL, 4>(a, B, lds, s);
 }
 
-template <int MODE, bool GV, bool XL = false>
+template <int MODE, bool GV, bool XL = false, bool SLICE = false>
 static void launch_solve(const SolveArgs& a, int B, int lds, hipStream_t s, int residual, int nw) {
-  if (residual == DAVA_RESIDUAL_RAY_ANGLE) launch_solve_res<MODE, GV, DAVA_RESIDUAL_RAY_ANGLE, XL>(a, B, lds, s, nw);
-  else launch_solve_res<MODE, GV, DAVA_RESIDUAL_SQUARED_REPROJECTION, XL>(a, B, lds, s, nw);
+  if (residual == DAVA_RESIDUAL_RAY_ANGLE) launch_solve_res<MODE, GV, DAVA_RESIDUAL_RAY_ANGLE, XL, SLICE>(a, B, lds, s, nw);
+  else launch_solve_res<MODE, GV, DAVA_RESIDUAL_SQUARED_REPROJECTION, XL, SLICE>(a, B, lds, s, nw);
 }
 
 // A recording solve (the tape of dava_tape.hpp) needs COMPACT mode and P <= 14336: the adjoint kernel
@@ -1855,7 +1900,7 @@ static bool tape_supported(const DavaScene* scene, const DavaSolverConfig* confi
 static TapeLayout solve_tape_layout(const DavaScene* scene, const DavaSolverConfig* config) {
   const int kcap = compact_capacity(config);
   const int Pv = round_up(scene->num_parameters, 4);
-  return tape_layout(scene->batch, scene->num_parameters, config->iterations, use_gv(scene, kcap) ? kVectors * Pv : 0);
+  return tape_layout(scene->batch, scene->num_parameters, config->iterations, use_gv(scene, kcap) ? gv_slice_floats(Pv, kcap, gv_slice_used(scene, kcap)) : 0);
 }
 
 static int solve_impl(const DavaScene* scene, const DavaSolverConfig* config, const float* x0, float* x_out,
@@ -1879,7 +1924,7 @@ static int solve_impl(const DavaScene* scene, const DavaSolverConfig* config, co
   const int lcap = mode == DAVA_HESSIAN_COMPACT ? lds_history_entries(scene, kcap, gv, nw) : 0;
   const int lds = lds_bytes_for(scene, kcap, gv, lcap, xl, nw);
   if (lds > kMaxLds) return DAVA_ERR_UNSUPPORTED;
-  const size_t vec = gv ? gv_vector_bytes(scene) : 0;
+  const size_t vec = gv ? gv_vector_bytes(scene, kcap) : 0;
   const TapeLayout tl = solve_tape_layout(scene, config);
   const size_t need = record ? tl.queue_byte : solve_state_bytes(scene, config);
   const bool uses_ws = record || gv || (mode == DAVA_HESSIAN_DENSE ? config->iterations > 2 : config->iterations > 1);
@@ -1899,6 +1944,9 @@ static int solve_impl(const DavaScene* scene, const DavaSolverConfig* config, co
   a.err_out = error_out;
   a.status = status_out;
   a.vecs = gv ? static_cast<float*>(workspace) : nullptr;
+  a.scal_slice = xl && gv_scalars_slice(scene, kcap) ? 1 : 0;
+  a.vstride = gv_slice_floats(round_up(scene->num_parameters, 4), kcap, a.scal_slice != 0);
+  a.kcap_lds = a.scal_slice ? 0 : kcap;
   a.hess = workspace ? reinterpret_cast<float*>(static_cast<char*>(workspace) + vec) : nullptr;
   a.hess_dense = hybrid && a.hess ? a.hess + compact_history_bytes(scene, config) / sizeof(float) : nullptr;
   a.c1 = config->sufficient_decrease;
@@ -1953,11 +2001,13 @@ static int solve_impl(const DavaScene* scene, const DavaSolverConfig* config, co
     else if (gv) launch_solve<DAVA_HESSIAN_DENSE, true>(a, scene->batch, lds, s, scene->residual, nw);
     else launch_solve<DAVA_HESSIAN_DENSE, false>(a, scene->batch, lds, s, scene->residual, nw);
   } else if (hybrid) {
-    if (xl) launch_solve<kHybrid, true, true>(a, scene->batch, lds, s, scene->residual, nw);
+    if (xl && a.scal_slice) launch_solve<kHybrid, true, true, true>(a, scene->batch, lds, s, scene->residual, nw);
+    else if (xl) launch_solve<kHybrid, true, true>(a, scene->batch, lds, s, scene->residual, nw);
     else if (gv) launch_solve<kHybrid, true>(a, scene->batch, lds, s, scene->residual, nw);
     else launch_solve<kHybrid, false>(a, scene->batch, lds, s, scene->residual, nw);
   } else {
-    if (xl) launch_solve<DAVA_HESSIAN_COMPACT, true, true>(a, scene->batch, lds, s, scene->residual, nw);
+    if (xl && a.scal_slice) launch_solve<DAVA_HESSIAN_COMPACT, true, true, true>(a, scene->batch, lds, s, scene->residual, nw);
+    else if (xl) launch_solve<DAVA_HESSIAN_COMPACT, true, true>(a, scene->batch, lds, s, scene->residual, nw);
     else if (gv) launch_solve<DAVA_HESSIAN_COMPACT, true>(a, scene->batch, lds, s, scene->residual, nw);
     else launch_solve<DAVA_HESSIAN_COMPACT, false>(a, scene->batch, lds, s, scene->residual, nw);
   }

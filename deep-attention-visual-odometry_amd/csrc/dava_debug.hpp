@@ -24,6 +24,7 @@ enum DebugKnob : int {
   kDbgAdjLdsEntries,  // >= 0: caps the adjoint's on-chip history entries
   kDbgAdjGdHbm,       // 1: the GV adjoint's dual gradient vector in HBM instead of LDS
   kDbgCompactSwitch,  // >= 1: COMPACT history capacity before the dense fold (default 1024; tests)
+  kDbgGvScalarSlice,  // 0 | 1: GV wide pass's rho_j, c_j in LDS / in the workspace slice (default: by fit)
   kDbgKnobs
 };
 

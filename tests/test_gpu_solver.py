@@ -452,6 +452,25 @@ def test_lds_staged_history_is_bitwise_the_register_pass(device, shape, override
     assert torch.equal(staged, regs) and torch.equal(st_staged, st_regs)
 
 
+@pytest.mark.parametrize("shape,k", [((2, 3600, False), 80), ((16, 4096, False), 70)])
+def test_gv_scalars_in_workspace_slice_are_bitwise_lds(device, shape, k, overrides):
+    """The global-vector pass reads each history entry's rho_j, c_j from LDS or -- when they would push the
+    XL image out of LDS (C5 past ~320 iterations) -- from the problem's workspace slice, 64 entries per
+    load and entry j's by readlane from lane j % 64 (wide_direction SLICE, rows of 6 or 7 float4 groups per
+    thread: P = 10,809 and 12,381 here).  The same values either way: forced both ways (GV_SCALAR_SLICE)
+    past a 64-entry chunk boundary, the two solves are bitwise equal."""
+    m, n, dist = shape
+    x0, obs, vis = _scene(2, m, n, dist, 971)
+    kw = dict(iterations=k, error_threshold=-1.0, minimum_step=-1.0, hessian_mode="compact")
+    overrides("FORCE_GV", 1)
+    overrides("GV_SCALAR_SLICE", 0)
+    lds, st_lds = _gpu_solve(device, x0, obs, vis, m, n, dist, **kw)
+    overrides("GV_SCALAR_SLICE", 1)
+    sl, st_sl = _gpu_solve(device, x0, obs, vis, m, n, dist, **kw)
+    assert torch.isfinite(lds).all() and (st_lds[:, 0] == k).all()
+    assert torch.equal(lds, sl) and torch.equal(st_lds, st_sl)
+
+
 @pytest.mark.parametrize("stopping", ["fixed", "reference"])
 def test_work_queue_launch_is_bitwise_invisible(device, stopping, overrides):
     """More problems than resident workgroups: with the work queue (a slot takes the next
