@@ -560,6 +560,30 @@ def test_gv_recording_is_bitwise_the_gv_solve(device, overrides):
     assert torch.equal(x, xr) and torch.equal(st, str_)
 
 
+def test_gv_recording_with_history_scalars_in_the_slice(device, overrides):
+    """The recording form of the solve kernel whose history scalars (rho_j, c_j) live in the workspace
+    slice (GV_SCALAR_SLICE, the kernel C5 runs past ~320 iterations; here P = 10,809, six float4 groups per
+    thread, K = 70 past a 64-entry boundary): the same x and status as the plain solve, bitwise, and the
+    gradient through it equals the LDS-scalar form's (the tape holds rho_j, c_j itself)."""
+    from deep_attention_visual_odometry_amd import make_scenes, native_ops
+
+    s = make_scenes(1, 2, 3600, distortion=False, seed=941, drop=0.0)
+    x0, obs, vis = (torch.tensor(t).to(device) for t in (s.initial, s.observations, s.visibility))
+    kw = dict(iterations=70, error_threshold=-1.0, minimum_step=-1.0)
+    w = torch.randn_like(x0)
+    out = {}
+    for tag, slice_ in (("slice", 1), ("lds", 0)):
+        overrides("GV_SCALAR_SLICE", slice_)
+        x, _, st = native_ops.ba_solve(x0, obs, vis, 2, 3600, False, hessian_mode=1, want_status=True, **kw)
+        xg = x0.clone().requires_grad_(True)
+        xr, str_ = native_ops.ba_solve_differentiable(xg, obs, vis, 2, 3600, False, **kw)
+        assert torch.equal(x, xr) and torch.equal(st, str_)
+        (gx,) = torch.autograd.grad((w * xr).sum(), xg)
+        out[tag] = (xr.detach(), gx)
+    assert torch.isfinite(out["slice"][1]).all()
+    assert torch.equal(out["slice"][0], out["lds"][0]) and torch.equal(out["slice"][1], out["lds"][1])
+
+
 @pytest.mark.parametrize("m,n,distortion,force_gv,k,b", [
     (4, 256, True, True, 8, 2),     # GV forward (forced) + GV adjoint, Brown-Conrady
     (4, 400, False, False, 10, 2),  # P = 1221 > 1024: LDS-mode forward, GV adjoint
