@@ -148,7 +148,12 @@ __host__ __device__ inline LdsCarve carve_lds(int M, int N, int Pv, int kcap = 0
   c.views = off; off += round_up(views_floats(M), 4);
   c.vpart = off; off += round_up(vpart_floats(M, nw), 4);
   c.scratch = off; off += 2 * nw * 32;
-  c.hcoef = off; off += 4 * kcap;  // COMPACT: per-entry product coefficients
+  // COMPACT: per-entry product coefficients, for the two-pass products only (compact_products: GV rows
+  // past the wide pass, LDS-mode rows of more than 4 float4 groups per lane); the single-pass forms form
+  // each entry's coefficients on the fly (r05: 16 B per entry returned to the on-chip history entries /
+  // the XL image)
+  const bool two_pass = gv ? !wide_history_pass(Pv, kcap, true) : (Pv / 4 + kWave - 1) / kWave > 4;
+  c.hcoef = off; off += two_pass ? 4 * kcap : 0;
   c.hrho = off; off += round_up(kcap, 4);
   c.hc = off; off += round_up(kcap, 4);
   c.hist = off; off += gv ? 0 : 2 * lcap * Pv;
@@ -1745,6 +1750,11 @@ static int lds_history_entries(const DavaScene* s, int kcap, bool gv, int nw) {
   int per_cu = 4 * kSolveWavesPerEU / nw;  // workgroups per CU at the register limit
   if (debug_knob(kDbgWgPerCu) > 0) per_cu = (int)debug_knob(kDbgWgPerCu);  // A/B: LDS budget = 160 KB / this
   int n = (kMaxLds / per_cu - base) / per;
+  // rows of <= 2 groups per lane consume the on-chip entries in batches, entries dealt round-robin to the
+  // waves: a multiple of the waves keeps the waves' batches equal (C2 at K = 100: 7 entries measured -1.2%
+  // against 6; the C1 shape 18 against 17 also -1.2%, so for these short rows an on-chip entry past the
+  // first few is worth little either way, profiles/r05_ab_lds_coefficients.log)
+  if ((Pv / 4 + kWave - 1) / kWave <= 2) n -= n % nw;
   if (debug_knob(kDbgLdsHistory) >= 0) n = (int)debug_knob(kDbgLdsHistory);
   n = min(n, (kMaxLds - base) / per);
   return max(0, min(n, kcap));
