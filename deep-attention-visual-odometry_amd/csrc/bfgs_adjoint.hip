@@ -52,6 +52,7 @@ struct AdjointArgs {
   int lcap;           // history entries (s_j, w_j), j < lcap, held in LDS for the H passes
   float* gvws;        // global-vector mode: (B, kAdjGvFloats(Pv)) per-problem vector slices, else null
   int gd_lds;         // global-vector mode: the HVP's dual gradient vector in LDS (carve_adjoint gdl)
+  int sc_global;      // LDS mode: the tape's scalar row read in place (bfgs_ba_adjoint_kernel SCG)
 };
 
 constexpr int kAdjWaves = 4;
@@ -412,9 +413,14 @@ __device__ __forceinline__ void wide_pair_pass(int P, int Pv, int j0, int j1, co
 // GT > 0: global-vector mode (the O(P) vectors in the workspace slice a.gvws, wide_pair_pass with up
 // to GT float4 groups per thread); GT = 0: everything O(P) in LDS (pair_pass, GM groups per lane).
 constexpr int kAdjLdsWpe = 2;
-template <int RES, int GM, int GT = 0, int NW = kAdjWaves>
+// SCG (LDS mode): the tape's scalar row (alpha_k, rho_j, c_j, gamma: about 4 K floats) read in place
+// instead of staged in LDS.  The row is sized by the iteration cap, not by the steps taken: at C3 with
+// the reference's default cap (1000) it pushed the image past the 80 KB that two workgroups per CU
+// need (profiles/r05_ab_adjoint_scalars.log).  A kernel of its own, as the forward's SLICE.
+template <int RES, int GM, int GT = 0, int NW = kAdjWaves, bool SCG = false>
 __global__ __launch_bounds__(kWave * NW, GT > 0 ? 1 : kAdjLdsWpe) void bfgs_ba_adjoint_kernel(AdjointArgs a) {
   static_assert(GT > 0 || NW == kAdjWaves, "LDS mode (pair_pass) runs four waves");
+  static_assert(!SCG || GT == 0, "SCG is an LDS-mode variant");
   constexpr int BLOCK = kWave * NW;
   extern __shared__ __attribute__((aligned(16))) float lds[];
   constexpr bool GVM = GT > 0;
@@ -422,7 +428,7 @@ __global__ __launch_bounds__(kWave * NW, GT > 0 ? 1 : kAdjLdsWpe) void bfgs_ba_a
   const int P = L.P, M = L.M, N = L.N, MN = M * N, Pv = a.Pv, K = a.K;
   const int b = blockIdx.x, tid = threadIdx.x;
   const TapeLayout& tl = a.tl;
-  const AdjointCarve cv = carve_adjoint(M, N, Pv, tl.T, a.lcap, GVM, NW, GVM && a.gd_lds);
+  const AdjointCarve cv = carve_adjoint(M, N, Pv, SCG ? 0 : tl.T, a.lcap, GVM, NW, GVM && a.gd_lds);
   float* vb = GVM ? a.gvws + (size_t)b * cv.gv_floats : lds;  // base of the O(P) vectors
   float* xb = vb + cv.xb;    // xbar: adjoint of x_{k+1} entering step k, of x_k leaving it
   float* sbp = vb + cv.sbp;  // adjoint of s_k from the update that used it (step k + 1)
@@ -449,7 +455,7 @@ __global__ __launch_bounds__(kWave * NW, GT > 0 ? 1 : kAdjLdsWpe) void bfgs_ba_a
   // workspace row a_k is written once, final, and only read by later steps (never read-modify-write)
   float* akl = vb + cv.ak;
   float* anl = vb + cv.an;
-  float* sc = lds + cv.sc;
+  const float* sc = SCG ? a.tape + tl.scal + (size_t)b * tl.T : lds + cv.sc;
   Dual* xd = reinterpret_cast<Dual*>(vb + cv.xd);
   Dual* gd = reinterpret_cast<Dual*>((GVM && a.gd_lds ? lds : vb) + cv.gd);
   // GV passes: the rows staged through the dual gradient vector's LDS slots (dead until the HVP)
@@ -473,7 +479,8 @@ __global__ __launch_bounds__(kWave * NW, GT > 0 ? 1 : kAdjLdsWpe) void bfgs_ba_a
     xb[i] = i < P ? a.xbar[(size_t)b * P + i] : 0.f;
     sbp[i] = gbp[i] = anl[i] = 0.f;
   }
-  for (int i = tid; i < tl.T; i += BLOCK) sc[i] = a.tape[tl.scal + (size_t)b * tl.T + i];
+  if constexpr (!SCG)
+    for (int i = tid; i < tl.T; i += BLOCK) lds[cv.sc + i] = a.tape[tl.scal + (size_t)b * tl.T + i];
   if constexpr (GVM) {
     if (obsacc)
       for (int i = tid; i < 2 * MN; i += BLOCK) obsacc[i] = 0.f;
@@ -661,6 +668,18 @@ static int adjoint_gv_waves(const DavaScene* s, const TapeLayout& tl) {
 
 template <int RES>
 static void launch_adjoint(const AdjointArgs& a, int B, int lds, int gm, int gt, int nw, hipStream_t s) {
+  if (gt == 0 && a.sc_global) {  // LDS mode, the tape's scalar row in place
+    auto go = [&](auto kernel) {
+      if (lds > 64 * 1024)
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+      hipLaunchKernelGGL(kernel, dim3(B), dim3(kAdjBlock), lds, s, a);
+    };
+    if (gm <= 1) go(bfgs_ba_adjoint_kernel<RES, 1, 0, kAdjWaves, true>);
+    else if (gm == 2) go(bfgs_ba_adjoint_kernel<RES, 2, 0, kAdjWaves, true>);
+    else if (gm == 3) go(bfgs_ba_adjoint_kernel<RES, 3, 0, kAdjWaves, true>);
+    else go(bfgs_ba_adjoint_kernel<RES, 4, 0, kAdjWaves, true>);
+    return;
+  }
   auto go = [&](auto kernel, int threads) {
     if (lds > 64 * 1024)
       (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize, lds);
@@ -707,11 +726,21 @@ static int adjoint_check(const DavaScene* s, const DavaSolverConfig* c) {
   return DAVA_OK;
 }
 
+// LDS mode: the tape's scalar row stays in place (SCG) when staging it would push the image past the two
+// workgroups per CU that the rest of it allows
+static bool adjoint_sc_global(const DavaScene* s, const TapeLayout& tl) {
+  if (adjoint_gv(s, tl)) return false;
+  if (debug_knob(kDbgAdjScGlobal) >= 0) return debug_knob(kDbgAdjScGlobal) > 0;  // tests
+  const int M = s->num_views, N = s->num_points;
+  return carve_adjoint(M, N, tl.Pv, tl.T).total_bytes > kAdjLdsBytes / kAdjLdsWpe &&
+         carve_adjoint(M, N, tl.Pv, 0).total_bytes <= kAdjLdsBytes / kAdjLdsWpe;
+}
+
 // As many history entries on chip as the CU's LDS leaves room for (one workgroup per CU), at most
 // the K - 1 a solve can make; the kDbgAdjLdsEntries override caps it (0: none) for A/B runs.  None in GV mode.
 static int adjoint_lds_entries(const DavaScene* s, const TapeLayout& tl) {
   if (adjoint_gv(s, tl)) return 0;
-  const int base = carve_adjoint(s->num_views, s->num_points, tl.Pv, tl.T).total_bytes;
+  const int base = carve_adjoint(s->num_views, s->num_points, tl.Pv, adjoint_sc_global(s, tl) ? 0 : tl.T).total_bytes;
   int n = (kAdjLdsBytes / kAdjLdsWpe - base) / (int)(2 * tl.Pv * sizeof(float));
   n = max(0, min(n, tl.K - 1));
   if (debug_knob(kDbgAdjLdsEntries) >= 0) n = max(0, min(n, (int)debug_knob(kDbgAdjLdsEntries)));
@@ -771,11 +800,13 @@ extern "C" int dava_ba_solve_backward(const DavaScene* scene, const DavaSolverCo
   a.arows = static_cast<float*>(workspace);
   a.gvws = gv ? reinterpret_cast<float*>(static_cast<char*>(workspace) + rows) : nullptr;
   a.lcap = adjoint_lds_entries(scene, tl);
+  a.sc_global = adjoint_sc_global(scene, tl) ? 1 : 0;
   const int nw = gv ? adjoint_gv_waves(scene, tl) : kAdjWaves;
   a.gd_lds = gv && !debug_flag(kDbgAdjGdHbm) &&
              carve_adjoint(scene->num_views, scene->num_points, tl.Pv, tl.T, a.lcap, gv, nw, true).total_bytes <=
                  kAdjLdsBytes;
-  const int lds = carve_adjoint(scene->num_views, scene->num_points, tl.Pv, tl.T, a.lcap, gv, nw, a.gd_lds).total_bytes;
+  const int lds = carve_adjoint(scene->num_views, scene->num_points, tl.Pv, a.sc_global ? 0 : tl.T, a.lcap, gv, nw,
+                                a.gd_lds).total_bytes;
   const int gm = (tl.Pv / 4 + kWave - 1) / kWave;
   const int gt = gv ? (tl.Pv / 4 + kWave * nw - 1) / (kWave * nw) : 0;  // float4 groups per thread
   hipStream_t s = static_cast<hipStream_t>(stream);

@@ -1766,11 +1766,11 @@ using namespace dava;
 
 // ---- debug overrides (dava_debug.hpp): set only through the two calls below, never from the environment ----
 namespace dava {
-static long long g_debug_knobs[kDbgKnobs] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};
+static long long g_debug_knobs[kDbgKnobs] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};
 static const char* const kDebugKnobNames[kDbgKnobs] = {
     "FORCE_GV", "GV_NO_XL", "SOLVE_WAVES", "WG_PER_CU", "LDS_HISTORY", "STAGGER", "STAGGER_LEVELS",
     "NO_PPT", "NO_QUEUE", "ADJ_GV_WAVES", "ADJ_FORCE_GV", "ADJ_LDS_ENTRIES", "ADJ_GD_HBM",
-    "COMPACT_SWITCH", "GV_SCALAR_SLICE"};
+    "COMPACT_SWITCH", "GV_SCALAR_SLICE", "ADJ_SC_GLOBAL"};
 long long debug_knob(int k) { return k >= 0 && k < kDbgKnobs ? g_debug_knobs[k] : -1; }
 }  // namespace dava
 

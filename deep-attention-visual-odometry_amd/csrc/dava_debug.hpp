@@ -25,6 +25,7 @@ enum DebugKnob : int {
   kDbgAdjGdHbm,       // 1: the GV adjoint's dual gradient vector in HBM instead of LDS
   kDbgCompactSwitch,  // >= 1: COMPACT history capacity before the dense fold (default 1024; tests)
   kDbgGvScalarSlice,  // 0 | 1: GV wide pass's rho_j, c_j in LDS / in the workspace slice (default: by fit)
+  kDbgAdjScGlobal,    // 0 | 1: LDS-mode adjoint's tape scalar row staged in LDS / read in place (default: by fit)
   kDbgKnobs
 };
 

@@ -27,7 +27,7 @@ LIB_PATH = (_DEBUG_ENV and os.environ.get("DAVA_LIB")) or os.path.join(_HERE, "_
 # Overridable launch choices of the library (csrc/dava_debug.hpp), and of this package's Python side
 LIBRARY_KNOBS = ("FORCE_GV", "GV_NO_XL", "SOLVE_WAVES", "WG_PER_CU", "LDS_HISTORY", "STAGGER", "STAGGER_LEVELS",
                  "NO_PPT", "NO_QUEUE", "ADJ_GV_WAVES", "ADJ_FORCE_GV", "ADJ_LDS_ENTRIES", "ADJ_GD_HBM",
-                 "COMPACT_SWITCH", "GV_SCALAR_SLICE")
+                 "COMPACT_SWITCH", "GV_SCALAR_SLICE", "ADJ_SC_GLOBAL")
 # GENERIC_BACKWARD: differentiate a fused objective's solve with the generic loop, not the adjoint;
 # GENERIC_TRAINING: training mode's drop path with the generic loop and torch's own RNG
 PYTHON_KNOBS = ("GENERIC_BACKWARD", "GENERIC_TRAINING")

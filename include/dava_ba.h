@@ -378,8 +378,9 @@ int dava_l1_camera_vjp_f64(int64_t batch, int32_t estimates, int32_t views, int3
  * on-chip history entries, work queue, ...) and reads NOTHING from the environment.  Tests and A/B
  * measurements override a choice by name (FORCE_GV, GV_NO_XL, SOLVE_WAVES, WG_PER_CU, LDS_HISTORY,
  * STAGGER, STAGGER_LEVELS, NO_PPT, NO_QUEUE, ADJ_GV_WAVES, ADJ_FORCE_GV, ADJ_LDS_ENTRIES, ADJ_GD_HBM,
- * COMPACT_SWITCH, GV_SCALAR_SLICE; csrc/dava_debug.hpp); value < 0 restores the library's choice.
- * Process-wide, not thread-safe, host-only.  DAVA_ERR_INVALID_ARGUMENT for an unknown name.      */
+ * COMPACT_SWITCH, GV_SCALAR_SLICE, ADJ_SC_GLOBAL; csrc/dava_debug.hpp); value < 0 restores the
+ * library's choice.  Process-wide, not thread-safe, host-only.  DAVA_ERR_INVALID_ARGUMENT for an
+ * unknown name.                                                                                   */
 int dava_debug_set_override(const char* name, int64_t value);
 void dava_debug_clear_overrides(void);
 

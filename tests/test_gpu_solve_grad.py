@@ -560,6 +560,28 @@ def test_gv_recording_is_bitwise_the_gv_solve(device, overrides):
     assert torch.equal(x, xr) and torch.equal(st, str_)
 
 
+@pytest.mark.parametrize("m,n,distortion", [(4, 256, True), (2, 128, False)])
+def test_adjoint_tape_scalars_in_place_are_bitwise_staged(device, m, n, distortion, overrides):
+    """The LDS-mode adjoint reads the tape's scalar row (alpha_k, rho_j, c_j, gamma) staged in LDS, or --
+    when staging it would cost the second workgroup per CU (long iteration caps) -- in place from the tape
+    (ADJ_SC_GLOBAL, a kernel of its own).  The same values either way: forced both ways, d (w . x) / d x0
+    and / d obs are bitwise equal."""
+    from deep_attention_visual_odometry_amd import make_scenes, native_ops
+
+    s = make_scenes(4, m, n, distortion=distortion, seed=951, drop=0.0)
+    x0, obs, vis = (torch.tensor(t).to(device) for t in (s.initial, s.observations, s.visibility))
+    kw = dict(iterations=20, error_threshold=-1.0, minimum_step=-1.0)
+    w = torch.randn_like(x0)
+    out = {}
+    for flag in (0, 1):
+        overrides("ADJ_SC_GLOBAL", flag)
+        xg, og = x0.clone().requires_grad_(True), obs.clone().requires_grad_(True)
+        xr, _ = native_ops.ba_solve_differentiable(xg, og, vis, m, n, distortion, **kw)
+        out[flag] = torch.autograd.grad((w * xr).sum(), [xg, og])
+    assert torch.isfinite(out[1][0]).all() and out[1][0].abs().max() > 0
+    assert torch.equal(out[0][0], out[1][0]) and torch.equal(out[0][1], out[1][1])
+
+
 def test_gv_recording_with_history_scalars_in_the_slice(device, overrides):
     """The recording form of the solve kernel whose history scalars (rho_j, c_j) live in the workspace
     slice (GV_SCALAR_SLICE, the kernel C5 runs past ~320 iterations; here P = 10,809, six float4 groups per
