@@ -101,14 +101,15 @@ constexpr int kGvEntries = DAVA_GV_ENTRIES;
 __host__ __device__ inline bool wide_history_pass(int Pv, int kcap, bool gv) {
   return gv && kcap > 0 && (Pv / 4 + kWave * solve_waves(gv) - 1) / (kWave * solve_waves(gv)) <= kWideMaxGroups;
 }
-// GV mode, wide pass: where each history entry's rho_j and c_j live.  In LDS (beside the product
-// coefficients, 24 B per entry) while the XL image (x, d and the objective's gradient, 149 KB at C5) still
-// fits beside them; past that (C5: ~320 iterations, e.g. the reference's default cap of 1000) in the
-// problem's workspace slice, after its kVectors vectors (round_up(kcap, 64) floats each), so that the XL
-// image stays: without it the solve ran at 4.80k against 7.22k problems/s at K = 100
-// (profiles/r05_ab_c5_xl.log); at K = 400 the slice form runs 689 against 539 problems/s, and K = 100
-// (LDS, as before) is unchanged (profiles/r05_ab_c5_scalar_slice.log).  The pass reads entry j's pair
-// with one uniform load each, issued at the entry's start and needed only after its block reduction.
+// GV mode, wide pass: where each history entry's rho_j and c_j live.  In LDS (8 B per entry) while the XL
+// image (x, d and the objective's gradient, 149 KB at C5) still fits beside them; past that (C5: ~950
+// iterations, e.g. the reference's default cap of 1000) in the problem's workspace slice, after its
+// kVectors vectors (round_up(kcap, 64) floats each), so that the XL image stays: without it the solve ran
+// at 4.80k against 7.22k problems/s at K = 100 (profiles/r05_ab_c5_xl.log).  Measured before the product
+// coefficients left the LDS image (when the slice took over at ~320 iterations): K = 400 689 against 539
+// problems/s, the reference's defaults 323 against 264, K = 100 unchanged (profiles/r05_ab_c5_scalar_slice.log).
+// The pass reads entry j's pair with one uniform load each, issued at the entry's start and needed only
+// after its block reduction.
 __host__ __device__ inline int gv_scalar_stride(int kcap) { return round_up(kcap, 64); }
 __host__ __device__ inline int gv_slice_floats(int Pv, int kcap, bool scalars_in_slice) {
   return kVectors * Pv + (scalars_in_slice ? 2 * gv_scalar_stride(kcap) : 0);
