@@ -27,6 +27,7 @@ K, CAP = 24, 8
     ((4, 256, True, 4), {"FORCE_GV": 1}),                     # global-vector mode, x and d in LDS
     ((4, 256, True, 4), {"FORCE_GV": 1, "GV_NO_XL": 1}),      # global-vector mode in place
     ((3, 1300, True, 2), {}),                                 # P = 3920: global-vector mode by size
+    ((2, 3600, False, 1), {"GV_SCALAR_SLICE": 1}),            # P = 10,809: rho_j, c_j in the workspace slice
 ])
 def test_hybrid_switch_matches_oracle(device, shape, knobs, overrides):
     """Capacity 8 at K = 24: 8 compact updates, the fold at iteration 9, 15 dense sweeps -- against the
