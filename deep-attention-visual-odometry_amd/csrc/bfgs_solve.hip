@@ -265,7 +265,8 @@ __device__ __forceinline__ void dense_sweep(const Layout& L, int Pld, float* __r
       return h;
     };
     int i = 0;
-    if (PIPE && materialized) {
+    // (the buffer descriptor's range is 32-bit: matrices past 2 GiB, P > 23,170, take the loop below)
+    if (PIPE && materialized && (size_t)P * Pld * sizeof(float) < (1ull << 31)) {
       // Global-vector mode (one problem per CU, rows of thousands of groups): software-pipelined,
       // two batches of U rows in flight per wave, through buffer loads / stores (a lane past the
       // wave's groups gets an offset past the descriptor's range: its load returns 0 and its store
@@ -276,7 +277,7 @@ __device__ __forceinline__ void dense_sweep(const Layout& L, int Pld, float* __r
       // C5 dense +4.9%; the LDS-mode kernels keep the predicated loop below: there (C3, two problems
       // per CU) the same change measured -2.8%, one batch ahead -0.4%, and 8 or 16 rows per batch
       // -0.4 / -2.7% (profiles/r05_ab_dense_sweep_pipe.log, r01_ab_sweep_variants.log).
-      const auto rs = make_rsrc(H, P * Pld * (int)sizeof(float));
+      const auto rs = make_rsrc(H, (int)((size_t)P * Pld * sizeof(float)));
       const unsigned rowb = (unsigned)Pld * 4u;
       const unsigned base = act ? (unsigned)j0 * 4u : 0x80000000u;
       auto ldrow = [&](int r) {
