@@ -73,10 +73,16 @@ def parse(argv=None):
                    help="problems of the first CPU slice whose per-block 1-ulp envelopes are computed (0 = skip)")
     p.add_argument("--cpu-sample", type=int, default=16,
                    help="problems per timed CPU-oracle run (3 runs on disjoint slices; 0 = skip)")
+    p.add_argument("--no-converged-parity", dest="converged_parity", action="store_false",
+                   help="skip parity.converged (the cpu_baseline problems solved by the reference's stopping rules on "
+                        "both sides; ~1 min of CPU)")
     p.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "pmc_traffic.json"))
-    p.add_argument("--entry", choices=["op", "module"], default="op",
+    p.add_argument("--entry", choices=["op", "module", "closure"], default="op",
                    help="module: time the drop-in BFGSSolver(...).eval()(x0, ReprojectionError) call itself "
-                        "(its own Hessian-mode choice and workspace allocation) instead of the op with a reused workspace")
+                        "(its own Hessian-mode choice and workspace allocation) instead of the op with a reused "
+                        "workspace; closure: the drop-in called as the reference's CalibrationNetwork calls it, with "
+                        "its torch error closure (networks/calibration_network.py:58-67, ray angle, pinhole), which "
+                        "runs the generic loop -- not the headline metric")
     p.add_argument("--differentiate", action="store_true",
                    help="time the solve AND its gradient (recording solve + adjoint kernel, d(w.x)/d(x0, obs)) -- "
                         "the reference's create_graph mode; not the headline metric")
@@ -216,6 +222,17 @@ def cpu_baseline(args, x0, obs, vis, x_gpu):
             nudged = solver.bfgs_solve(torch.nextafter(x0[:m], torch.full_like(x0[:m], to)), closure(0, m), **kw)
             for key, sl in (("x", slice(None)), ("i", slice(0, 3)), ("d", slice(-5, None))):
                 spread[key] = torch.maximum(spread[key], _rel(nudged[:, sl], ref[:m, sl]))
+        noise = ulp_noise_spread(solver, x0[:m], closure(0, m), kw, ref[:m])
+        parity["over_per_evaluation_ulp_noise"] = {
+            k: {"max": float((r[:m] / noise[key].clamp(min=1e-300)).max()),
+                "median": float((r[:m] / noise[key].clamp(min=1e-300)).median()),
+                "spread_max": float(noise[key].max())}
+            for k, key, r in (("whole", "x", rel), ("intrinsics", "i", rel_i),
+                              ("distortion", "d", _rel(gpu[:, -5:], ref[:, -5:])))}
+        parity["over_per_evaluation_ulp_noise"]["note"] = (
+            "the GPU's distance from the oracle over the oracle's own spread when EVERY objective value and iterate "
+            "gradient it sees moves by -1/0/+1 ulp at random (max over 2 seeds; oracle.solver ulp_noise) -- the "
+            "perturbation a reordered fp32 sum makes in every evaluation, where the x0 nudge perturbs the start only")
         env = {k: torch.clamp(ENVELOPE_FACTOR * v, min=PARITY_BAR) for k, v in spread.items()}
         rel_d = _rel(gpu[:, -5:], ref[:, -5:])
 
@@ -238,6 +255,8 @@ def cpu_baseline(args, x0, obs, vis, x_gpu):
             "distortion_envelope_min": float(env["d"].min()),
             "distortion_max_rel_over_envelope": float((rel_d[:m] / env["d"]).max()),
             "envelope_factor": ENVELOPE_FACTOR,
+            "envelope_factor_source": "tests/golden/parity_envelope.json (derived there from the committed ratio "
+                                      "distributions; tests/test_bench_cpu.py asserts the two agree)",
             "note": ("per-block envelopes = max(1e-5, envelope_factor x the oracle's own change under a 1-ulp nudge of x0); "
                      "*_over_1ulp = the GPU's distance / that change (1x, no floor): <= 1 means no farther from the "
                      "oracle than the reference is from itself under a 1-ulp nudge; the "
@@ -245,7 +264,71 @@ def cpu_baseline(args, x0, obs, vis, x_gpu):
                      "(tests/golden/distortion.npz), whose own eager and TorchScript runs differ on k1..p2 by up to "
                      "~1e-3 at K=100"),
         })
+    if args.converged_parity and args.residual == "reprojection" and args.error_threshold < 0:
+        parity["converged"] = converged_parity(args, x0[: 3 * n], obs[: 3 * n], vis[: 3 * n],
+                                               closure, args.parity_envelope, x_gpu.device)
     return cpu, parity
+
+
+BLOCKS = (("x", slice(None)), ("i", slice(0, 3)), ("d", slice(-5, None)))
+
+
+def ulp_noise_spread(solver, x0, closure, kw, ref, seeds=(1, 2)):
+    """Per problem and block, the oracle's largest distance from its own result `ref` when every evaluation it
+    sees carries random 1-ulp noise (oracle.solver.bfgs_solve ulp_noise), over `seeds`."""
+    out = {k: torch.zeros((x0.shape[0],), dtype=torch.float64) for k, _ in BLOCKS}
+    for seed in seeds:
+        noisy = solver.bfgs_solve(x0, closure, ulp_noise=torch.Generator().manual_seed(seed), **kw)
+        for key, sl in BLOCKS:
+            out[key] = torch.maximum(out[key], _rel(noisy[:, sl], ref[:, sl]))
+    return out
+
+
+def converged_parity(args, x0, obs, vis, closure, n_env, dev):
+    """north_star's 'converged camera parameters ... within 1e-5 rel': the reference's stopping rules
+    (error 1e-4, 1000 iterations, step 1e-8: bfgs_solver.py:53-55) on the cpu_baseline problems, the fused solve
+    against the oracle run the same way.  Per camera parameter (f, cx, cy, k1..p2): max |rel| and the fraction of
+    problems within 1e-5; per block: the GPU's distance over the oracle's own spread (1-ulp nudge of x0 up/down,
+    and per-evaluation ulp noise) on the first n_env problems, and the stop iterations / reasons compared."""
+    from deep_attention_visual_odometry_amd import _native, native_ops
+    from oracle import solver
+
+    kw = dict(iterations=1000, error_threshold=1e-4, minimum_step=1e-8)
+    n = x0.shape[0]
+    x_g, _, st = native_ops.ba_solve(x0.to(dev), obs[:n].to(dev), vis[:n].to(dev, dtype=torch.uint8), args.views,
+                                     args.points, not args.no_distortion, hessian_mode=_native.DAVA_HESSIAN_COMPACT,
+                                     want_status=True, **kw)
+    x_g, st = x_g.cpu(), st.cpu()
+    rec = solver.SolveRecord(iterations=None, reason=None)
+    ref = torch.cat([solver.bfgs_solve(x0[lo:lo + 16], closure(lo, min(lo + 16, n)), record=(rec if lo == 0 else None),
+                                       **kw) for lo in range(0, n, 16)])
+    names = ["f", "cx", "cy"] + (["k1", "k2", "k3", "p1", "p2"] if not args.no_distortion else [])
+    cols = list(range(3)) + (list(range(x0.shape[1] - 5, x0.shape[1])) if not args.no_distortion else [])
+    per = {}
+    for name, c in zip(names, cols):
+        r = ((x_g[:, c] - ref[:, c]).abs().double() / ref[:, c].abs().double().clamp(min=1e-30))
+        per[name] = {"max_rel": float(r.max()), "frac_le_1e-5": float((r <= PARITY_BAR).double().mean())}
+    m = min(n_env, n, 16)
+    spread = {k: torch.zeros((m,), dtype=torch.float64) for k, _ in BLOCKS}
+    for to in (float("inf"), -float("inf")):
+        nudged = solver.bfgs_solve(torch.nextafter(x0[:m], torch.full_like(x0[:m], to)), closure(0, m), **kw)
+        for key, sl in BLOCKS:
+            spread[key] = torch.maximum(spread[key], _rel(nudged[:, sl], ref[:m, sl]))
+    noise = ulp_noise_spread(solver, x0[:m], closure(0, m), kw, ref[:m])
+    blocks = {}
+    for name, key, sl in (("whole", "x", slice(None)), ("intrinsics", "i", slice(0, 3)), ("distortion", "d", slice(-5, None))):
+        if key == "d" and args.no_distortion:
+            continue
+        r = _rel(x_g[:, sl], ref[:, sl])
+        blocks[name] = {"max_rel": float(r.max()), "frac_le_1e-5": float((r <= PARITY_BAR).double().mean()),
+                        "over_1ulp_nudge_max": float((r[:m] / spread[key].clamp(min=1e-300)).max()),
+                        "over_ulp_noise_max": float((r[:m] / noise[key].clamp(min=1e-300)).max()),
+                        "nudge_spread_max": float(spread[key].max()), "noise_spread_max": float(noise[key].max())}
+    return {"n": n, "rules": "error_threshold 1e-4, iterations 1000, minimum_step 1e-8 (bfgs_solver.py:53-55)",
+            "per_parameter": per, "blocks": blocks, "envelope_problems": m,
+            "same_stop_iteration": float((st[:16, 0] == rec.iterations.to(st.dtype)).double().mean()),
+            "same_stop_reason": float((st[:16, 1] == rec.reason.to(st.dtype)).double().mean()),
+            "mean_iterations": float(st[:, 0].double().mean())}
 
 
 def _scenes(args, b, first, distortion, ray):
@@ -342,6 +425,20 @@ def main():
                 x = module(x0, fn)
                 return x, module.last_status
 
+        if args.entry == "closure":  # the reference's unchanged caller: a torch closure, the generic loop
+            if not ray or distortion:
+                raise SystemExit("--entry closure is CalibrationNetwork's ray-angle error: add --residual ray_angle "
+                                 "--no-distortion")
+            from deep_attention_visual_odometry_amd import BFGSSolver
+            from deep_attention_visual_odometry_amd.geometry import calibration_network_error
+
+            fn = calibration_network_error(obs, vis.to(obs.dtype), args.views, args.points)
+            module = BFGSSolver(error_threshold=args.error_threshold, iterations=args.iterations,
+                                minimum_step=args.minimum_step).eval()
+
+            def solve():  # noqa: F811
+                return module(x0, fn), torch.zeros((b, 4), dtype=torch.int32, device=dev)
+
         if args.differentiate:  # recording solve + adjoint, each timed with its own events
             cot = torch.randn(x0.shape, generator=torch.Generator().manual_seed(1)).to(dev)
             phase_ms = []
@@ -396,6 +493,8 @@ def main():
     if world > 1:
         dist.barrier()
     sync()
+    if not launch_test:
+        torch.cuda.reset_peak_memory_stats(dev)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         x, status, gathered = step(True)
@@ -409,8 +508,9 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
     ranks = per_rank_phases(kernel_ms, gather_ms, world, dev) if world > 1 else None
+    peak_bytes = None if launch_test else int(torch.cuda.max_memory_allocated(dev))
     sustained = None
-    if args.sustain_seconds > 0 and not launch_test and not args.differentiate:
+    if args.sustain_seconds > 0 and not launch_test and not args.differentiate and args.entry != "closure":
         sustained = sustain(args, solve, sync, elapsed / args.steps, world, b, dev)
 
     if gathered is not None:  # diagnostics over the whole global batch
@@ -442,6 +542,9 @@ def main():
         elif args.differentiate:
             print(json.dumps(differentiate_line(args, base, world, b, p, distortion, ray, phase_ms[-args.steps:],
                                                 st, finite, solve.grads)), flush=True)
+        elif args.entry == "closure":
+            print(json.dumps(closure_line(args, base, world, b, p, x0, obs, vis, x, module, peak_bytes, finite)),
+                  flush=True)
         else:
             line = measurement_line(args, base, world, b, p, mn, distortion, ray, plan, kernel_ms, st, finite, x0_cpu,
                                     obs_cpu, vis_cpu, x)
@@ -490,6 +593,13 @@ def _config_argv(args):
     return out + (["--no-distortion"] if args.no_distortion else [])
 
 
+def _child_argv(args):
+    """The command line of a counter-pass child: ONE launch of this configuration, no warm-up, no CPU oracle, no
+    counter passes or sustained phase of its own (a 10 s phase under rocprofv3 --pmc would profile ~300 launches)."""
+    return [sys.executable, os.path.abspath(__file__), "--steps", "1", "--warmup", "0", "--cpu-sample", "0",
+            "--no-live-counters", "--sustain-seconds", "0"] + _config_argv(args)
+
+
 def live_traffic(args, kernel="bfgs_ba_solve_kernel"):
     """HBM (fabric) bytes per launch of the solve kernel, measured in THIS run: two rocprofv3 --pmc passes
     (FETCH_SIZE, then WRITE_SIZE: they cannot share a pass) over a child bench process that runs one launch of
@@ -508,9 +618,7 @@ def live_traffic(args, kernel="bfgs_ba_solve_kernel"):
     with tempfile.TemporaryDirectory(prefix="dava_pmc_", dir="/tmp") as tmp:
         for counter in ("FETCH_SIZE", "WRITE_SIZE"):
             out = os.path.join(tmp, counter)
-            cmd = [prof, "--pmc", counter, "-d", out, "-o", "p", "--output-format", "csv", "--",
-                   sys.executable, os.path.abspath(__file__), "--steps", "1", "--warmup", "0", "--cpu-sample", "0",
-                   "--no-live-counters", "--sustain-seconds", "0"] + _config_argv(args)
+            cmd = [prof, "--pmc", counter, "-d", out, "-o", "p", "--output-format", "csv", "--"] + _child_argv(args)
             env = dict(os.environ, TMPDIR="/tmp")
             try:
                 r = subprocess.run(cmd, cwd="/tmp", env=env, capture_output=True, text=True, timeout=180)
@@ -675,6 +783,52 @@ def differentiate_line(args, line, world, b, p, distortion, ray, phase_ms, st, f
     return line
 
 
+def closure_line(args, line, world, b, p, x0, obs, vis, x, module, peak_bytes, finite):
+    """--entry closure: the drop-in BFGSSolver called with the reference's own torch closure (generic loop)."""
+    from deep_attention_visual_odometry_amd import _native, native_ops
+
+    hist = getattr(module, "last_generic_history", None)
+    # the same problems through the fused kernel (RayAngleError): how far the generic loop's result is from it
+    x_f, _, _ = native_ops.ba_solve(x0, obs, vis, args.views, args.points, False, iterations=args.iterations,
+                                    error_threshold=args.error_threshold, minimum_step=args.minimum_step,
+                                    hessian_mode=_native.DAVA_HESSIAN_COMPACT,
+                                    residual=_native.DAVA_RESIDUAL_RAY_ANGLE)
+    rel = _rel(x.detach().cpu(), x_f.cpu())
+    line.update({
+        "metric": f"BA problems/sec through the drop-in BFGSSolver called as CalibrationNetwork calls it: its torch "
+                  f"error closure (networks/calibration_network.py:58-67, ray angle), B={b}, {args.views} views x "
+                  f"{args.points} pts, K={args.iterations} -- the generic loop, not the headline metric",
+        "dtype": "f32",
+        "data": "synthetic (seeded look-at scenes, noise-free observations, x0 = truth + noise)",
+        "config": {"workload": f"closure: batch={b}, {args.views}x{args.points}, P={p}, K={args.iterations}"
+                               f"{' fixed iterations' if args.error_threshold < 0 else ' max, reference stopping rules'}",
+                   "global_batch": world * b, "num_parameters": p, "iterations": args.iterations,
+                   "parallelism": f"dp{world}"},
+        "generic_inverse_hessian": "compact history (dava_bfgs_compact_direction)" if hist is not None else
+                                   "dense (B, P, P), the reference's data structure",
+        "peak_memory_bytes": peak_bytes,
+        "history_bytes": hist.nbytes() if hist is not None else None,
+        "roofline": None,
+        "cpu_baseline": None,
+        "parity": {"vs_fused_ray_angle_solve_max_rel": float(rel.max()), "median_rel": float(rel.median()),
+                   "note": "the fused RayAngleError solve of the same problems (its parity with the oracle: "
+                           "tests/test_gpu_solver.py); the closure's own parity with the oracle: tests/test_gpu_generic.py"},
+        "diagnostics": {"all_finite": finite},
+    })
+    return line
+
+
+def status_percentiles(st):
+    """Per-problem distribution of the status words (steps, objective evaluations, line-search trials): a launch of
+    one workgroup per problem lasts as long as its slowest problems, so the tail matters beside the mean."""
+    out = {}
+    for col, name in ((0, "steps"), (2, "evaluations"), (3, "trials")):
+        v = st[:, col].double()
+        q = torch.quantile(v, torch.tensor([0.5, 0.9, 0.99], dtype=torch.float64)).tolist()
+        out[name] = {"mean": round(v.mean().item(), 2), "p50": q[0], "p90": q[1], "p99": q[2], "max": v.max().item()}
+    return out
+
+
 def measurement_line(args, line, world, b, p, mn, distortion, ray, plan, kernel_ms, st, finite, x0_cpu, obs_cpu,
                      vis_cpu, x):
     fixed_k = args.error_threshold < 0 and args.minimum_step < 0  # every problem runs exactly K iterations
@@ -790,6 +944,7 @@ def measurement_line(args, line, world, b, p, mn, distortion, ray, plan, kernel_
         "diagnostics": {"objective_evals_per_iteration": round(evals, 3),
                         "line_search_trials_per_iteration": round(trials, 3),
                         "mean_steps_per_problem": round(st[:, 0].double().mean().item(), 2),
+                        "per_problem": status_percentiles(st),
                         "problems_in_diagnostics": int(st.shape[0]),
                         "all_finite": finite, "plan": plan},
     })

@@ -107,6 +107,153 @@ __global__ __launch_bounds__(kBlock) void search_direction_kernel(int64_t n, con
   }
 }
 
+// ---- compact-history search direction for the generic loop (r06) ----
+// The generic loop (any closure) used to keep the reference's dense (B, P, P) inverse Hessian and gather /
+// scatter it with the active-problem mask every iteration (bfgs_solver.py:157-180).  This op keeps the same
+// rank-2 terms as history rows instead -- the fused solve's COMPACT form, exact BFGS in product form:
+//   H' v = gamma v + sum_{j < count} [c_j rho_j (s_j . v) - rho_j (w_j . v)] s_j - rho_j (s_j . v) w_j
+// and one launch per iteration does, for every active problem r (history slot b = idx[r]):
+//   count == 0: gamma = clamp(s.y / clamp(y.y, 1e-5), 1e-4) (bfgs_solver.py:217-233), stored in gamma[b];
+//   H'y, H'g from the stored entries (pass 1: each wave reduces its entries' four dots into coefficients in
+//   LDS; pass 2: column-parallel accumulation, every row read once more);
+//   rho = 1/(s.y) (0 if s.y <= 0, func_inverse_curvature.py:24-28), c = 1 + rho y.H'y;
+//   d = -H g with H = H' + c rho s s^T - rho s (H'y)^T - rho (H'y) s^T (the fused kernel's formula order);
+//   appends entry `count` = (s, H'y, rho, c).
+// Memory O(count P) per problem instead of O(P^2); bytes per iteration 2 x 8 count Pv instead of the dense
+// path's ~5 x 4 P^2.  Rows: S, W (B, cap, Pv); rho, c (B, cap); g, y, s, d (n_active, P) contiguous.
+template <typename T>
+__device__ __forceinline__ T block_sum_n(T v, T* red) {
+  const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
+  v = wave_sum(v);
+  __syncthreads();
+  if (lane == 0) red[wave] = v;
+  __syncthreads();
+  T t = red[0];
+  for (int w = 1; w < (int)(blockDim.x / kWave); ++w) t += red[w];
+  return t;
+}
+
+template <typename T>
+__global__ __launch_bounds__(kBlock) void compact_direction_kernel(int64_t P, int64_t Pv, int64_t cap, int64_t count,
+                                                                  const int64_t* __restrict__ idx,
+                                                                  const T* __restrict__ g, const T* __restrict__ y,
+                                                                  const T* __restrict__ s, T* S, T* W, T* rho, T* cc,
+                                                                  T* gamma, T* __restrict__ d) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  T* yl = reinterpret_cast<T*>(smem);
+  T* gl = yl + Pv;
+  T* coef = gl + Pv;  // 4 per entry: (a_y, b_y, a_g, b_g)
+  __shared__ T red[kWaves];
+  const int64_t r = blockIdx.x;
+  const int64_t b = idx[r];
+  const int tid = threadIdx.x, lane = tid & (kWave - 1), wave = tid / kWave;
+  const T* gr = g + r * P;
+  const T* yr = y + r * P;
+  const T* sr = s + r * P;
+  T* dr = d + r * P;
+  T* Sb = S + b * cap * Pv;
+  T* Wb = W + b * cap * Pv;
+  for (int64_t i = tid; i < P; i += kBlock) {
+    yl[i] = yr[i];
+    gl[i] = gr[i];
+  }
+  __syncthreads();
+  // pass 1: per entry, the four dots (s_j.y, s_j.g, w_j.y, w_j.g) -> coefficients, entries dealt to waves
+  for (int64_t j = wave; j < count; j += kWaves) {
+    const T* sj = Sb + j * Pv;
+    const T* wj = Wb + j * Pv;
+    T sy = 0, sg = 0, wy = 0, wg = 0;
+    for (int64_t i = lane; i < P; i += kWave) {
+      const T a = sj[i], w = wj[i], yi = yl[i], gi = gl[i];
+      sy += a * yi; sg += a * gi; wy += w * yi; wg += w * gi;
+    }
+    sy = wave_sum(sy); sg = wave_sum(sg); wy = wave_sum(wy); wg = wave_sum(wg);
+    if (lane == 0) {
+      const T rj = rho[b * cap + j], cj = cc[b * cap + j];
+      coef[4 * j + 0] = cj * rj * sy - rj * wy;
+      coef[4 * j + 1] = -rj * sy;
+      coef[4 * j + 2] = cj * rj * sg - rj * wg;
+      coef[4 * j + 3] = -rj * sg;
+    }
+  }
+  T gm;
+  if (count == 0) {  // H_0 = gamma I (bfgs_solver.py:159-167)
+    T sy = 0, yy = 0;
+    for (int64_t i = tid; i < P; i += kBlock) { sy += sr[i] * yl[i]; yy += yl[i] * yl[i]; }
+    sy = block_sum_n(sy, red);
+    yy = block_sum_n(yy, red);
+    gm = clamp_min(sy / clamp_min(yy, T(1e-5)), T(1e-4));
+    if (tid == 0) gamma[b] = gm;
+  } else {
+    __syncthreads();  // coefficients complete
+    gm = gamma[b];
+  }
+  // pass 2: H'y and H'g column by column (consecutive threads read consecutive columns of every row); H'y is
+  // the new entry's w row, H'g is parked in d until the curvature sums are known
+  T* wn = Wb + count * Pv;
+  T* sn = Sb + count * Pv;
+  T r0 = 0, r1 = 0, r2 = 0, r3 = 0;
+  for (int64_t i = tid; i < P; i += kBlock) {
+    const T yi = yl[i], gi = gl[i], si = sr[i];
+    T hy = gm * yi, hg = gm * gi;
+    int64_t j = 0;
+    for (; j + 4 <= count; j += 4) {  // four entries' loads in flight
+      T a[4], w[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) { a[u] = Sb[(j + u) * Pv + i]; w[u] = Wb[(j + u) * Pv + i]; }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const T* cf = coef + 4 * (j + u);
+        hy += cf[0] * a[u] + cf[1] * w[u];
+        hg += cf[2] * a[u] + cf[3] * w[u];
+      }
+    }
+    for (; j < count; ++j) {
+      const T a = Sb[j * Pv + i], w = Wb[j * Pv + i];
+      const T* cf = coef + 4 * j;
+      hy += cf[0] * a + cf[1] * w;
+      hg += cf[2] * a + cf[3] * w;
+    }
+    wn[i] = hy;
+    sn[i] = si;
+    dr[i] = hg;
+    r0 += si * yi; r1 += hy * yi; r2 += si * gi; r3 += hy * gi;
+  }
+  for (int64_t i = P + tid; i < Pv; i += kBlock) { wn[i] = 0; sn[i] = 0; }
+  r0 = block_sum_n(r0, red);
+  r1 = block_sum_n(r1, red);
+  r2 = block_sum_n(r2, red);
+  r3 = block_sum_n(r3, red);
+  const T rh = r0 <= T(0) ? T(0) : T(1) / r0;
+  const T c = T(1) + rh * r1;
+  const T sg = r2, hyg = r3, rsg = rh * sg;
+  for (int64_t i = tid; i < P; i += kBlock) {  // (each thread reads back what it wrote)
+    const T sri = sr[i] * rh;
+    dr[i] = T(-1) * (dr[i] + sri * (c * sg) - sri * hyg - wn[i] * rsg);
+  }
+  if (tid == 0) {
+    rho[b * cap + count] = rh;
+    cc[b * cap + count] = c;
+  }
+}
+
+template <typename T>
+int compact_direction(int64_t n_active, int64_t P, int64_t Pv, int64_t cap, int64_t count, const int64_t* idx,
+                      const T* g, const T* y, const T* s, T* S, T* W, T* rho, T* c, T* gamma, T* d, void* stream) {
+  if (n_active < 0 || P < 1 || Pv < P || count < 0 || count >= cap) return DAVA_ERR_INVALID_ARGUMENT;
+  if (n_active == 0) return DAVA_OK;
+  if (!idx || !g || !y || !s || !S || !W || !rho || !c || !gamma || !d) return DAVA_ERR_INVALID_ARGUMENT;
+  const size_t lds = (2 * (size_t)Pv + 4 * (size_t)count) * sizeof(T);
+  if (lds > 150 * 1024) return DAVA_ERR_UNSUPPORTED;
+  const auto kernel = compact_direction_kernel<T>;
+  if (lds > 64 * 1024)
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)lds);
+  hipLaunchKernelGGL(kernel, dim3((unsigned)n_active), dim3(kBlock), lds, static_cast<hipStream_t>(stream), P, Pv,
+                     cap, count, idx, g, y, s, S, W, rho, c, gamma, d);
+  return hipGetLastError() == hipSuccess ? DAVA_OK : DAVA_ERR_LAUNCH;
+}
+
 // state columns
 enum { S_ALO = 0, S_AHI, S_A, S_FLO, S_FHI, S_FA, S_DFA, S_F0, S_DPHI0, S_COLS };
 
@@ -294,6 +441,20 @@ extern "C" int dava_bfgs_search_direction_f32(int64_t batch, int64_t n, const fl
 extern "C" int dava_bfgs_search_direction_f64(int64_t batch, int64_t n, const double* h, const double* g,
                                               double* d_out, void* stream) {
   return search_direction<double>(batch, n, h, g, d_out, stream);
+}
+extern "C" int dava_bfgs_compact_direction_f32(int64_t n_active, int64_t n, int64_t row_stride, int64_t capacity,
+                                               int64_t count, const int64_t* problem_index, const float* g,
+                                               const float* y, const float* s, float* S, float* W, float* rho,
+                                               float* c, float* gamma, float* d_out, void* stream) {
+  return compact_direction<float>(n_active, n, row_stride, capacity, count, problem_index, g, y, s, S, W, rho, c,
+                                  gamma, d_out, stream);
+}
+extern "C" int dava_bfgs_compact_direction_f64(int64_t n_active, int64_t n, int64_t row_stride, int64_t capacity,
+                                               int64_t count, const int64_t* problem_index, const double* g,
+                                               const double* y, const double* s, double* S, double* W, double* rho,
+                                               double* c, double* gamma, double* d_out, void* stream) {
+  return compact_direction<double>(n_active, n, row_stride, capacity, count, problem_index, g, y, s, S, W, rho, c,
+                                   gamma, d_out, stream);
 }
 extern "C" int dava_wolfe_init_f32(int64_t batch, int64_t n, const float* direction, const float* f0, const float* g0,
                                    float* state, uint8_t* flags, void* stream) {

@@ -23,7 +23,9 @@
 //    never stored (the first sweep synthesises it).
 //  * the line search runs in-kernel; trial slopes come from forward-mode
 //    (JVP) derivatives, gradients at accepted points from reverse mode.
+#include <algorithm>
 #include <cstring>
+#include <vector>
 
 #include "ba_objective.hpp"
 #include "dava_debug.hpp"
@@ -178,6 +180,23 @@ constexpr int kSweepRows = 4;  // DENSE sweep: matrix rows in flight per lane
 // global-vector mode, where it saves the pair sweep's tangent registers (C5 +4%, r03 interleaved A/B).
 constexpr bool kTrialDotLds = false;
 constexpr bool kTrialDotGv = true;
+// Lean trials (LDS mode, r06): only a line search's first trial forms the reverse-mode gradient.  Every
+// later trial (widening or zoom) is evaluated for E and the forward-mode slope alone -- all the Wolfe tests
+// read (wolfe_conditions.py:116-237) -- and, if it is the one accepted, the next iteration evaluates the
+// gradient at x_{k+1} instead of reusing the trial's.  The alpha sequence is bitwise unchanged (the same E
+// and slope arithmetic, reduced in the same order).  GV mode keeps its reverse-mode trial slope (d . grad,
+// kTrialDotGv), whose rounding the forward-mode slope would not reproduce.
+// DAVA_LEAN_TRIALS: the first trial index evaluated lean (0: none).
+#ifndef DAVA_LEAN_TRIALS
+#define DAVA_LEAN_TRIALS 1
+#endif
+constexpr int kLeanFrom = DAVA_LEAN_TRIALS;
+constexpr bool kLeanTrials = kLeanFrom > 0;
+// Runs of known no-move zoom trials iterated as the scalar recurrence they are (r06; bitwise invisible).
+#ifndef DAVA_NOMOVE_RUNS
+#define DAVA_NOMOVE_RUNS 1
+#endif
+constexpr bool kNoMoveRuns = DAVA_NOMOVE_RUNS != 0;
 constexpr int kSolveWavesPerEU = 2;  // <= 256 VGPRs: two 4-wave workgroups per CU
 // Diagnostic builds only (make variant FLAGS=-DDAVA_PHASE_TIMING=1): thread 0 of every
 // workgroup accumulates shader-clock cycles per solver phase; dava_ba_solve prints the
@@ -1423,6 +1442,7 @@ __global__ __launch_bounds__(kWave * NW, kSolveWavesPerEU) void bfgs_ba_solve_ke
       // problems: thousands per solve).
       float nomove_al = -1.0f;
       bool widen = true, zoom = false, evaluated = false, last_same = false;
+      bool last_grad = false;  // the last evaluated trial formed its gradient (reusable at x_{k+1})
       // trial gradients go into gp's buffer (g_prev is dead once d is formed)
       const float lim = (-a.c2) * dphi0;
       for (int t = 0; t < a.max_trials; ++t) {
@@ -1437,14 +1457,57 @@ __global__ __launch_bounds__(kWave * NW, kSolveWavesPerEU) void bfgs_ba_solve_ke
         // return f(x) and, via autograd w.r.t. alpha, (d * g).sum() -- exactly f0 and
         // phi'(0).  The check rides on the objective's first reduction (CHECK).  Otherwise
         // E and the full gradient at the trial point are formed (kept for reuse as the
-        // next iterate's gradient) and phi'(alpha) = d . grad (DOT).
+        // next iterate's gradient) and phi'(alpha) = d . grad (DOT) -- for the first trial;
+        // later ones form E and phi'(alpha) only (kLeanTrials).
         const bool known_same = al <= nomove_al;  // uniform
-        if (!known_same &&
-            ba_eval<true, !kTrialDot, true, kTrialDot, true, RES, float, NW, PPT,
-                    GV>(
-                L, x, d, al, obs, vis, grad_buf(gp), views, vpart, scratch, buf, fa, dfa)) {
+        if (kNoMoveRuns && known_same && zoom && E >= f_lo) {
+          // A run of known no-move trials in the zoom phase: each trial point is x itself (f = E, phi' =
+          // phi'(0)), and with E >= f_lo every one fails the sufficient-decrease test, so a_hi <- alpha and
+          // the next bisection point is tried.  That is a scalar recurrence: iterate it here, without the
+          // trial machinery, until the interval closes, the next point needs an evaluation (above
+          // nomove_al) or the trial budget ends -- the same states and counts as the general path below,
+          // trial by trial (uniform; C2's slowest problems run thousands of these per solve).
+          for (;;) {
+            a_hi = al;
+            f_hi = E;
+            ++trials;
+            if (a_lo == a_hi) { zoom = false; break; }
+            if (t + 1 >= a.max_trials) break;
+            const float nx = 0.5f * (a_lo + a_hi);
+            if (!(nx <= nomove_al)) break;
+            al = nx;
+            ++t;
+          }
+          evaluated = true;
+          last_same = true;
+          last_al = al;
+          last_fa = fa = E;
+          dfa = dphi0;
+          continue;
+        }
+        constexpr bool kLean = kLeanTrials && !kTrialDot;
+        const bool lean = kLean && t >= kLeanFrom;  // uniform
+        bool moved = false;
+        if (!known_same) {
+          if (lean)
+            moved = ba_eval<false, true, true, false, true, RES, float, NW, PPT, GV>(
+                L, x, d, al, obs, vis, nullptr, views, vpart, scratch, buf, fa, dfa);
+          else
+            moved = ba_eval<true, !kTrialDot, true, kTrialDot, true, RES, float, NW, PPT, GV>(
+                L, x, d, al, obs, vis, grad_buf(gp), views, vpart, scratch, buf, fa, dfa);
+        }
+        if (moved) {
           ++evals;
           last_same = false;
+          last_grad = !lean;
+          if (kLean && lean && !(isfinite(fa) && isfinite(dfa))) {
+            // overflowed lean trial: the rule below needs the reverse-mode gradient (rare; the same point,
+            // so the same E)
+            ba_eval<true, true, true, false, false, RES, float, NW, PPT, GV>(L, x, d, al, obs, vis, grad_buf(gp), views,
+                                                                      vpart, scratch, buf, fa, dfa);
+            ++evals;
+            last_grad = true;
+          }
           // Overflowed trial (fp32 at a wild step): the reference's phi'(alpha) is autograd w.r.t.
           // alpha, i.e. (grad E(x + alpha d) * d).sum() (wolfe_conditions.py:134-143) -- NaN as
           // soon as the reverse-mode gradient holds a NaN or infinities of both signs, where the
@@ -1498,7 +1561,7 @@ __global__ __launch_bounds__(kWave * NW, kSolveWavesPerEU) void bfgs_ba_solve_ke
       }
       const float alpha = a_hi;
       if (a.tape_s && tid == 0) a.tape_s[(size_t)b * a.tape_T + k] = alpha;
-      have_next = evaluated && last_al == alpha;
+      have_next = evaluated && last_al == alpha && (last_same || last_grad);
       E_next = last_fa;
       if (have_next && last_same) {  // x_{k+1} == x_k bitwise: its gradient is g itself
         for (int i = tid; i < P; i += BLOCK) gp[i] = g[i];
@@ -1641,6 +1704,9 @@ __global__ __launch_bounds__(kWave * NW) void ba_evaluate_kernel(EvalArgs a) {
     for (int i = tid; i < P; i += BLOCK) a.grad[(size_t)b * P + i] = g[i];
 }
 
+// ---- host API (everything below): left out of the microbenchmarks that include this file for its device
+// passes alone (tools/micro/*.hip define DAVA_DEVICE_PASSES_ONLY), so they do not instantiate every solve kernel
+#ifndef DAVA_DEVICE_PASSES_ONLY
 static int check_scene(const DavaScene* s, bool need_data = true) {
   if (!s) return DAVA_ERR_INVALID_ARGUMENT;
   if (s->batch < 0 || s->num_views < 2 || s->num_points < 1) return DAVA_ERR_INVALID_ARGUMENT;
@@ -2038,6 +2104,19 @@ static int solve_impl(const DavaScene* scene, const DavaSolverConfig* config, co
     fprintf(stderr, "[dava phase cycles / problem]");
     for (int i = 0; i < kPhases; ++i) fprintf(stderr, " %s=%.0f (%.1f%%)", names[i], avg[i], 100.0 * avg[i] / avg[kPhases - 1]);
     fprintf(stderr, "\n");
+    // per-problem distribution (a launch lasts as long as its slowest problems): p50 / p99 / max per phase
+    {
+      std::vector<unsigned long long> col(scene->batch);
+      fprintf(stderr, "[dava phase cycles distribution]");
+      for (int i = 0; i < kPhases; ++i) {
+        for (int b = 0; b < scene->batch; ++b) col[b] = h[(size_t)b * kPhases + i];
+        std::sort(col.begin(), col.end());
+        const size_t n = col.size();
+        fprintf(stderr, " %s=p50:%llu,p99:%llu,max:%llu", names[i], col[n / 2], col[std::min(n - 1, (size_t)(0.99 * n))],
+                col[n - 1]);
+      }
+      fprintf(stderr, "\n");
+    }
     unsigned long long ev[kEvalSections] = {};
     (void)hipMemcpyFromSymbol(ev, HIP_SYMBOL(g_eval_cycles), sizeof(ev));
     static const char* enames[kEvalSections] = {"view_constants", "point_sums", "setup", "pair_sweep", "final_sums",
@@ -2131,3 +2210,7 @@ extern "C" int dava_ba_evaluate(const DavaScene* scene, const float* x, const fl
   else launch_eval<false, false, false>(a, B, lds, s, form, scene->residual);
   return hipGetLastError() == hipSuccess ? DAVA_OK : DAVA_ERR_LAUNCH;
 }
+
+#else
+}  // namespace dava
+#endif  // DAVA_DEVICE_PASSES_ONLY

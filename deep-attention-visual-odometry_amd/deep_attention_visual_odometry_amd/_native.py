@@ -29,8 +29,9 @@ LIBRARY_KNOBS = ("FORCE_GV", "GV_NO_XL", "SOLVE_WAVES", "WG_PER_CU", "LDS_HISTOR
                  "NO_PPT", "NO_QUEUE", "ADJ_GV_WAVES", "ADJ_FORCE_GV", "ADJ_LDS_ENTRIES", "ADJ_GD_HBM",
                  "COMPACT_SWITCH", "GV_SCALAR_SLICE", "ADJ_SC_GLOBAL")
 # GENERIC_BACKWARD: differentiate a fused objective's solve with the generic loop, not the adjoint;
-# GENERIC_TRAINING: training mode's drop path with the generic loop and torch's own RNG
-PYTHON_KNOBS = ("GENERIC_BACKWARD", "GENERIC_TRAINING")
+# GENERIC_TRAINING: training mode's drop path with the generic loop and torch's own RNG;
+# GENERIC_DENSE: the generic loop keeps the reference's dense (B, P, P) inverse Hessian even without a graph
+PYTHON_KNOBS = ("GENERIC_BACKWARD", "GENERIC_TRAINING", "GENERIC_DENSE")
 _py_knobs = {k: -1 for k in PYTHON_KNOBS}
 
 DAVA_OK = 0
@@ -124,6 +125,7 @@ for _t in ("f32", "f64"):
         f"dava_bfgs_initial_scale_{_t}": (ctypes.c_int, [_c_i64, _c_i64, _vp, _vp, _vp, _vp]),
         f"dava_bfgs_scale_matrix_{_t}": (ctypes.c_int, [_c_i64, _c_i64, _vp, _vp, _vp, _vp]),
         f"dava_bfgs_search_direction_{_t}": (ctypes.c_int, [_c_i64, _c_i64, _vp, _vp, _vp, _vp]),
+        f"dava_bfgs_compact_direction_{_t}": (ctypes.c_int, [_c_i64] * 5 + [_vp] * 11),
         f"dava_wolfe_init_{_t}": (ctypes.c_int, [_c_i64, _c_i64, _vp, _vp, _vp, _vp, _vp, _vp]),
         f"dava_wolfe_propose_{_t}": (ctypes.c_int, [_c_i64, _vp, _vp, _vp]),
         f"dava_wolfe_update_{_t}": (ctypes.c_int, [_c_i64, _c_i32, _scalar, _scalar, _c_i32, _vp, _vp, _vp]),

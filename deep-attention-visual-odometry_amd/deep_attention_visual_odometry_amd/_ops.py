@@ -448,6 +448,46 @@ def _(h, g):
     return torch.empty_like(g)
 
 
+@torch.library.custom_op("dava::bfgs_compact_direction",
+                         mutates_args=("history_s", "history_w", "history_rho", "history_c", "gamma"),
+                         device_types=_CUDA)
+def bfgs_compact_direction(g: Tensor, y: Tensor, s: Tensor, problem_index: Tensor, count: int, history_s: Tensor,
+                           history_w: Tensor, history_rho: Tensor, history_c: Tensor, gamma: Tensor) -> Tensor:
+    """The generic loop's update + search direction on compact history rows (no dense matrix): appends
+    entry ``count`` to the history of the problems ``problem_index`` and returns d = -H g (n_active, P)."""
+    n_act, p = _row_batch(g, "gradient")
+    _same(y, g, (n_act, p), "delta_gradient")
+    _same(s, g, (n_act, p), "step")
+    if problem_index.dtype != torch.int64 or tuple(problem_index.shape) != (n_act,) \
+            or problem_index.device != g.device or not problem_index.is_contiguous():
+        raise ValueError("problem_index must be a contiguous int64 (n_active,) tensor on the gradient's device")
+    if history_s.dim() != 3 or history_w.shape != history_s.shape or history_s.dtype != g.dtype \
+            or history_w.dtype != g.dtype or history_s.shape[2] < p:
+        raise ValueError("history rows must be (B, capacity, >= P) in the gradient's dtype")
+    b_all, cap, stride = history_s.shape
+    for t, shape, what in ((history_rho, (b_all, cap), "history_rho"), (history_c, (b_all, cap), "history_c"),
+                           (gamma, (b_all,), "gamma")):
+        if tuple(t.shape) != shape or t.dtype != g.dtype:
+            raise ValueError(f"{what} must be {shape} in the gradient's dtype")
+    for t in (history_s, history_w, history_rho, history_c, gamma):
+        if not t.is_contiguous() or t.device != g.device:
+            raise ValueError("history tensors must be contiguous and on the gradient's device")
+    if not 0 <= count < cap:
+        raise ValueError(f"count {count} outside the history capacity {cap}")
+    out = torch.empty_like(g)
+    with torch.cuda.device(g.device):
+        N.check(getattr(N.load_library(), f"dava_bfgs_compact_direction_{_dt(g)}")(
+            n_act, p, stride, cap, count, N.ptr(problem_index), N.ptr(g), N.ptr(y), N.ptr(s), N.ptr(history_s),
+            N.ptr(history_w), N.ptr(history_rho), N.ptr(history_c), N.ptr(gamma), N.ptr(out),
+            N.stream_of(g.device)), "dava_bfgs_compact_direction")
+    return out
+
+
+@bfgs_compact_direction.register_fake
+def _(g, y, s, problem_index, count, history_s, history_w, history_rho, history_c, gamma):
+    return torch.empty_like(g)
+
+
 @torch.library.custom_op("dava::bfgs_search_direction_backward", mutates_args=(), device_types=_CUDA)
 def bfgs_search_direction_backward(h: Tensor, g: Tensor, grad: Tensor, need_h: bool,
                                    need_g: bool) -> Tuple[Tensor, Tensor]:

@@ -261,9 +261,22 @@ class BFGSSolver(Module):
         step = torch.zeros_like(parameters)
         error = torch.empty(batch_dimensions, dtype=parameters.dtype, device=device)
         gradient = torch.empty_like(parameters)
-        inverse_hessian = torch.zeros(batch_dimensions + (parameter_dim, parameter_dim), dtype=parameters.dtype,
-                                      device=device)
-        inverse_hessian[..., range(parameter_dim), range(parameter_dim)] = 1.0
+        # The inverse Hessian: compact history rows on the device when no graph is kept (r06: no (B, P, P)
+        # matrix, no masked gather / scatter of it; native_ops.CompactHistory), else the reference's dense
+        # matrix, whose ops carry the VJP kernels the create_graph mode needs (and the host flavours on CPU).
+        history = None
+        if (not create_graph and device.type == "cuda" and self.hessian_mode != "dense"
+                and not _native.python_knob("GENERIC_DENSE")
+                and native_ops.CompactHistory.supported(parameter_dim, parameters.dtype, num_iterations - 1)):
+            n_problems = max(int(torch.tensor(batch_dimensions).prod().item()) if len(batch_dimensions) else 1, 1)
+            history = native_ops.CompactHistory(n_problems, parameter_dim, parameters.dtype, device,
+                                                max_entries=num_iterations - 1)
+            inverse_hessian = None
+        else:
+            inverse_hessian = torch.zeros(batch_dimensions + (parameter_dim, parameter_dim), dtype=parameters.dtype,
+                                          device=device)
+            inverse_hessian[..., range(parameter_dim), range(parameter_dim)] = 1.0
+        self.last_generic_history = history
         for step_idx in range(num_iterations):
             prev_gradient = gradient
             if self.training and self.drop_path_p > 0.0:
@@ -284,6 +297,10 @@ class BFGSSolver(Module):
             upd_grad = gradient[updating]
             if step_idx == 0:
                 direction = -1.0 * upd_grad
+            elif history is not None:
+                active = torch.nonzero(updating.reshape(-1)).squeeze(1)  # flat problem indices, batch order
+                direction = history.direction(upd_grad, upd_grad - prev_gradient[updating], step[updating],
+                                              active).reshape(upd_grad.shape)
             else:
                 delta = upd_grad - prev_gradient[updating]
                 upd_h = inverse_hessian[updating]

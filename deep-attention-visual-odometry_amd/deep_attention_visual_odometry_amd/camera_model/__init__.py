@@ -15,6 +15,7 @@ from typing import NamedTuple
 import torch
 
 from .. import native_ops
+from ..geometry.closure_ops import get_camera_relative_points  # noqa: F401  (reference: camera_model/__init__.py)
 
 
 def num_parameters(num_views: int, num_points: int, distortion: bool = False) -> int:

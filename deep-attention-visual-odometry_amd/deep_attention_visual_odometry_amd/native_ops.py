@@ -320,6 +320,58 @@ def search_direction(h: torch.Tensor, g: torch.Tensor) -> torch.Tensor:
     return _SearchDirection.apply(h, g)
 
 
+class CompactHistory:
+    """The generic loop's inverse Hessian as compact history rows (``dava_bfgs_compact_direction``): per problem
+    of the whole batch the rank-2 terms (s_j, w_j = H_{j-1} y_j, rho_j, c_j) and gamma, replacing the reference's
+    dense (B, P, P) matrix and its masked gather / scatter (``bfgs_solver.py:157-180``).  Rows grow by doubling
+    as the loop runs, so memory is O(k P) per problem at iteration k.  Not differentiable: the loop takes it
+    only when no graph is kept (the create_graph mode keeps the dense ops and their VJP kernels)."""
+
+    LDS_LIMIT = 150 * 1024  # csrc/bfgs_ops.hip compact_direction: y, g and 4 coefficients per entry in LDS
+
+    def __init__(self, batch: int, p: int, dtype: torch.dtype, device, max_entries: int, capacity: int = 16):
+        self.batch, self.p, self.dtype, self.device = int(batch), int(p), dtype, device
+        self.stride = (self.p + 3) // 4 * 4
+        self.max_entries = max(int(max_entries), 1)
+        self.count = 0
+        self.gamma = torch.zeros((self.batch,), dtype=dtype, device=device)
+        self._alloc(min(capacity, self.max_entries))
+
+    @classmethod
+    def supported(cls, p: int, dtype: torch.dtype, max_entries: int) -> bool:
+        if dtype not in (torch.float32, torch.float64):
+            return False
+        size = 4 if dtype == torch.float32 else 8
+        return (2 * ((p + 3) // 4 * 4) + 4 * max(max_entries, 1)) * size <= cls.LDS_LIMIT
+
+    def _alloc(self, cap: int) -> None:
+        new = [torch.zeros((self.batch, cap, self.stride), dtype=self.dtype, device=self.device) for _ in range(2)]
+        scal = [torch.zeros((self.batch, cap), dtype=self.dtype, device=self.device) for _ in range(2)]
+        if self.count:
+            for a, b in zip(new + scal, (self.s, self.w, self.rho, self.c)):
+                a[:, :self.count] = b[:, :self.count]
+        self.s, self.w = new
+        self.rho, self.c = scal
+        self.capacity = cap
+
+    def direction(self, gradient: torch.Tensor, delta_gradient: torch.Tensor, step: torch.Tensor,
+                  problem_index: torch.Tensor) -> torch.Tensor:
+        """Append (step, H'y) for the active problems `problem_index` (flat batch indices, int64) and return
+        d = -H g for them, H the inverse Hessian after this update."""
+        if self.count >= self.max_entries:
+            raise RuntimeError(f"compact history full ({self.max_entries} entries)")
+        if self.count >= self.capacity:
+            self._alloc(min(2 * self.capacity, self.max_entries))
+        d = torch.ops.dava.bfgs_compact_direction(_c(gradient.detach()), _c(delta_gradient.detach()),
+                                                  _c(step.detach()), _c(problem_index), self.count, self.s, self.w,
+                                                  self.rho, self.c, self.gamma)
+        self.count += 1
+        return d
+
+    def nbytes(self) -> int:
+        return sum(t.numel() * t.element_size() for t in (self.s, self.w, self.rho, self.c, self.gamma))
+
+
 class WolfeState:
     """Device-resident batched line-search state (columns per include/dava_ba.h)."""
     A_LO, A_HI, A, F_LO, F_HI, F_A, DPHI_A, F0, DPHI0 = range(9)

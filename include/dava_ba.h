@@ -169,8 +169,9 @@ int dava_ba_solve_record(const DavaScene* scene, const DavaSolverConfig* config,
 size_t dava_ba_solve_backward_workspace_bytes(const DavaScene* scene, const DavaSolverConfig* config);
 
 /* History entries (s_j, w_j) the adjoint keeps in LDS for its whole reverse sweep (the oldest
- * ones, as many as one workgroup's LDS leaves room for, at most iterations - 1; the
- * DAVA_ADJ_LDS_ENTRIES environment variable caps it).  Informational: for byte models. */
+ * ones, as many as one workgroup's LDS leaves room for, at most iterations - 1).  The library
+ * reads no environment; only the test/A-B override dava_debug_set_override("ADJ_LDS_ENTRIES", n)
+ * caps it.  Informational: for byte models. */
 int dava_ba_solve_backward_lds_entries(const DavaScene* scene, const DavaSolverConfig* config);
 
 /* Vector-Jacobian product of the recorded solve: given x_out_grad = dL/dx_out (B, P), writes
@@ -231,6 +232,25 @@ int dava_bfgs_search_direction_f32(int64_t batch, int64_t n, const float* h, con
                                    void* stream);
 int dava_bfgs_search_direction_f64(int64_t batch, int64_t n, const double* h, const double* g,
                                    double* d_out, void* stream);
+
+/* The generic loop's update + direction WITHOUT the dense matrix (bfgs_solver.py:157-180, the
+ * reference's gather / update / scatter of a (B, P, P) inverse Hessian): the inverse Hessian is kept
+ * as compact history rows, exact BFGS in product form (the fused solve's COMPACT mode).
+ *   S, W   (B_all, capacity, row_stride) history rows s_j and w_j = H_{j-1} y_j of every problem;
+ *   rho, c (B_all, capacity); gamma (B_all): per-problem scalars (gamma written when count == 0);
+ *   problem_index (n_active) int64: the history slot of each active row of g, y, s, d_out (n_active, n);
+ *   count: entries stored so far (the same for every active problem: the loop's step index - 1).
+ * For each active problem: H' = gamma I + the `count` stored rank-2 terms; appends entry `count`
+ * = (s, H'y, 1/(s.y) or 0 if s.y <= 0, 1 + rho y.H'y) and writes d_out = -H g for
+ * H = H' + the new term.  Needs count < capacity and row_stride >= n. */
+int dava_bfgs_compact_direction_f32(int64_t n_active, int64_t n, int64_t row_stride, int64_t capacity,
+                                    int64_t count, const int64_t* problem_index, const float* g, const float* y,
+                                    const float* s, float* S, float* W, float* rho, float* c, float* gamma,
+                                    float* d_out, void* stream);
+int dava_bfgs_compact_direction_f64(int64_t n_active, int64_t n, int64_t row_stride, int64_t capacity,
+                                    int64_t count, const int64_t* problem_index, const double* g, const double* y,
+                                    const double* s, double* S, double* W, double* rho, double* c,
+                                    double* gamma, double* d_out, void* stream);
 
 /* Strong/weak Wolfe line-search state machine (wolfe_conditions.py:23-239),
  * batched, for an error function evaluated by the caller between calls.

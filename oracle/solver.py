@@ -149,6 +149,21 @@ def wolfe_line_search(
     return a_hi
 
 
+def ulp_jitter(t: torch.Tensor, gen: torch.Generator) -> torch.Tensor:
+    """t with every element moved by -1, 0 or +1 ulp (uniformly at random from `gen`)."""
+    sign = torch.randint(0, 3, t.shape, generator=gen) - 1
+    up = torch.nextafter(t, torch.full_like(t, float("inf")))
+    down = torch.nextafter(t, torch.full_like(t, -float("inf")))
+    return torch.where(sign > 0, up, torch.where(sign < 0, down, t))
+
+
+def _jittered_closure(closure, gen: torch.Generator):
+    def fn(x: torch.Tensor, mask: torch.Tensor) -> torch.Tensor:
+        out = closure(x, mask)
+        return out + (ulp_jitter(out.detach(), gen) - out.detach())  # the value moves, its gradient does not
+    return fn
+
+
 @dataclass
 class SolveRecord:
     iterations: torch.Tensor  # int, steps applied per problem
@@ -171,6 +186,7 @@ def bfgs_solve(
     training: bool = False,
     drop_path_p: float = 0.0,
     return_second_last: bool = False,
+    ulp_noise: Optional[torch.Generator] = None,
 ) -> torch.Tensor:
     """Eval-mode ``BFGSSolver.forward`` (``bfgs_solver.py:80-215``).
     ``trajectory`` (optional list) receives x after every iteration's step.
@@ -181,8 +197,14 @@ def bfgs_solve(
     threshold / iteration count): per-iteration drop-path ``active &= rand_like > p``
     (``:121-125``, drawn with ``torch.rand_like`` so a test can make it deterministic) and
     ``return_second_last`` (``:196-212``), including the reference's scatter of the
-    previous active set's rows into the smaller new active set."""
+    previous active set's rows into the smaller new active set.
+    ``ulp_noise`` (a generator; parity diagnostics only, never for the goldens): every objective value the
+    solve sees (the iterate's and every line-search trial's) and every gradient at an iterate move by -1, 0
+    or +1 ulp at random -- the oracle's own spread under a last-bit change in EVERY evaluation, which is
+    what a reordered fp32 sum does, where the 1-ulp nudge of x0 perturbs the start only."""
     create_graph = x0.requires_grad
+    if ulp_noise is not None:
+        closure = _jittered_closure(closure, ulp_noise)
     x = x0 if create_graph else x0.detach()
     shape = x.shape[:-1]
     p = x.size(-1)
@@ -212,6 +234,8 @@ def bfgs_solve(
         with torch.enable_grad():
             fa = closure(xa, active)
             (ga,) = torch.autograd.grad(fa.sum(), xa, create_graph=create_graph)
+        if ulp_noise is not None:
+            ga = ulp_jitter(ga.detach(), ulp_noise)
         calls[0] += 1
         err = err.masked_scatter(active, fa.detach())
         grad = grad.masked_scatter(active.unsqueeze(-1).expand_as(grad), ga)

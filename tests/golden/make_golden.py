@@ -761,11 +761,34 @@ def gen_c5():
             np.savez_compressed(os.path.join(HERE, "c5_traj.npz"), **out)
 
 
+def gen_c5_eight():
+    """As gen_c5, K = 20 only, on the bench's first EIGHT C5 problems (r06: the per-block parity at C5 pinned
+    on more than two problems).  Only x0 is stored beside the results: the scenes are regenerated from the
+    seed (make_scenes), and the test checks that x0 matches.  ~4 min per run here, three runs."""
+    import time
+
+    m, n = 16, 4096
+    s = make_scenes(8, m, n, distortion=False, seed=20251015 + 3000)
+    x0, obs, vis = torch.tensor(s.initial), torch.tensor(s.observations), torch.tensor(s.visibility)
+    out = {"x0": x0.numpy()}
+    fn = closure_for(obs, vis, m, n)
+    starts = {"": x0, "_up": torch.nextafter(x0, torch.full_like(x0, float("inf"))),
+              "_down": torch.nextafter(x0, torch.full_like(x0, -float("inf")))}
+    for tag, start in starts.items():
+        t = time.time()
+        res = BFGSSolver(iterations=20, error_threshold=-1.0, minimum_step=-1.0).eval()(start, fn)
+        out[f"k20{tag}"] = res.numpy()
+        print(f"c5x8 K=20{tag}: {time.time() - t:.0f} s", flush=True)
+        np.savez_compressed(os.path.join(HERE, "c5_traj8.npz"), **out)
+
+
 if __name__ == "__main__":
     torch.set_num_threads(8)
     which = sys.argv[1:] or ["eval", "update", "ls", "traj", "ray", "grad", "train", "l1", "l1grad", "bc", "bcmask"]
     if "c5" in which:  # not in the default set: ~1 h of CPU
         gen_c5()
+    if "c5x8" in which:  # not in the default set: ~12 min of CPU
+        gen_c5_eight()
     if "bc" in which:
         gen_distortion()
     if "bcmask" in which:

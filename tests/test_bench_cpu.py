@@ -37,7 +37,21 @@ def test_sustained_phase_runs_the_step_for_its_budget(bench):
 def test_child_runs_skip_the_sustained_phase(bench):
     args = bench.parse(["--batch", "256", "--views", "16", "--points", "4096", "--no-distortion"])
     assert args.sustain_seconds == 10.0  # the default run carries the phase
-    src = open(os.path.join(REPO, "bench.py")).read()
-    assert '"--sustain-seconds", "0"' in src  # the rocprofv3 child passes of live_traffic skip it
     argv = bench._config_argv(args)
     assert "--no-distortion" in argv and "4096" in argv
+    child = bench._child_argv(args)  # what live_traffic runs under rocprofv3 --pmc
+    assert child[child.index("--sustain-seconds") + 1] == "0"
+    assert "--no-live-counters" in child
+    assert child[child.index("--steps") + 1] == "1" and child[child.index("--cpu-sample") + 1] == "0"
+    assert child[-len(argv):] == argv  # the same configuration
+    again = bench.parse(child[2:])  # and it parses back to this configuration
+    assert (again.batch, again.views, again.points, again.no_distortion) == (256, 16, 4096, True)
+    assert again.sustain_seconds == 0 and again.no_live_counters
+
+
+def test_status_percentiles(bench):
+    st = torch.zeros((100, 4), dtype=torch.int32)
+    st[:, 2] = torch.arange(100)
+    out = bench.status_percentiles(st)
+    assert out["evaluations"]["max"] == 99 and out["evaluations"]["p50"] == pytest.approx(49.5)
+    assert out["steps"]["max"] == 0 and set(out) == {"steps", "evaluations", "trials"}

@@ -436,3 +436,126 @@ def test_training_mode_uses_training_threshold_and_iterations(device):
     trained = solver(x0, rosenbrock)
     evald = solver.eval()(x0, rosenbrock)
     assert rosenbrock(evald).item() < rosenbrock(trained).item()
+
+
+# ---- the generic loop's compact history (r06: dava_bfgs_compact_direction, no (B, P, P) matrix) ----
+
+def _dense_reference_directions(g_seq, y_seq, s_seq):
+    """d_k from the dense building blocks exactly as the reference's loop forms them (bfgs_solver.py:157-176):
+    H_0 = I scaled by gamma at k = 1, then the rank-2 update and d = -H g, for k = 1 .. len."""
+    from deep_attention_visual_odometry_amd import native_ops
+
+    b, n = g_seq[0].shape
+    h = torch.eye(n, dtype=g_seq[0].dtype, device=g_seq[0].device).expand(b, n, n).contiguous()
+    out = []
+    for k, (g, y, s) in enumerate(zip(g_seq, y_seq, s_seq)):
+        if k == 0:
+            h = native_ops.scale_matrix(native_ops.initial_scale(s, y), h)
+        h = native_ops.update_inverse_hessian(h, s, y)
+        out.append(native_ops.search_direction(h, g))
+    return out
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.float64, 1e-10), (torch.float32, 1e-5)])
+def test_compact_direction_matches_the_dense_update(device, dtype, tol, fixed_random_seed):
+    """The op's d after k updates equals the dense matrix's d (same rank-2 terms, product form): 6 problems,
+    n = 37, 12 iterations, one update with s.y <= 0 (skipped by rho = 0 in both forms)."""
+    from deep_attention_visual_odometry_amd import native_ops
+
+    b, n, iters = 6, 37, 12
+    a = torch.randn(b, n, n, dtype=torch.float64)
+    spd = (a @ a.transpose(1, 2) / n + torch.eye(n, dtype=torch.float64)).to(dtype).to(device)
+    g_seq, y_seq, s_seq = [], [], []
+    for k in range(iters):
+        s = torch.randn(b, n, dtype=dtype, device=device)
+        y = torch.einsum("bij,bj->bi", spd, s)
+        if k == 5:
+            y[2] = -y[2]  # negative curvature for problem 2 at this step
+        g_seq.append(torch.randn(b, n, dtype=dtype, device=device))
+        y_seq.append(y)
+        s_seq.append(s)
+    want = _dense_reference_directions(g_seq, y_seq, s_seq)
+    hist = native_ops.CompactHistory(b, n, dtype, device, max_entries=iters, capacity=2)  # grows 2 -> 4 -> 8 -> 12
+    idx = torch.arange(b, device=device)
+    for k in range(iters):
+        d = hist.direction(g_seq[k], y_seq[k], s_seq[k], idx)
+        rel = ((d - want[k]).norm(dim=-1) / want[k].norm(dim=-1)).max().item()
+        assert rel <= tol, (k, rel)
+    assert hist.count == iters and hist.capacity == iters
+    assert hist.rho[2, 5].item() == 0.0 and bool((hist.rho[:, :iters] != 0).sum() == b * iters - 1)
+
+
+def test_compact_direction_touches_only_the_active_problems(device, fixed_random_seed):
+    """Rows of problems outside problem_index keep their history bit for bit (the mask contract: a stopped
+    problem's inverse Hessian is never updated, bfgs_solver.py:178-180)."""
+    from deep_attention_visual_odometry_amd import native_ops
+
+    b, n = 5, 20
+    hist = native_ops.CompactHistory(b, n, torch.float32, device, max_entries=4)
+    all_idx = torch.arange(b, device=device)
+    r = lambda m: torch.randn(m, n, device=device)  # noqa: E731
+    hist.direction(r(b), r(b).abs(), r(b).abs(), all_idx)
+    before = [t.clone() for t in (hist.s, hist.w, hist.rho, hist.c, hist.gamma)]
+    active = torch.tensor([0, 3], device=device)
+    hist.direction(r(2), r(2).abs(), r(2).abs(), active)
+    for t0, t1 in zip(before, (hist.s, hist.w, hist.rho, hist.c, hist.gamma)):
+        for i in (1, 2, 4):
+            assert torch.equal(t0[i], t1[i])
+    assert not torch.equal(before[0][0], hist.s[0])
+
+
+@pytest.mark.parametrize("fn,x0", [(rosenbrock, [[1.5, -2.0], [-1.2, 1.0], [0.3, 0.4]]),
+                                   (wavy, [[0.7, -0.2, 1.1], [2.0, 0.1, -0.5], [-0.3, 0.9, 0.2]])])
+def test_generic_loop_compact_matches_dense(device, fn, x0):
+    """The whole generic loop (reference stopping rules, masks) with the compact history vs the dense matrix
+    (the GENERIC_DENSE override), fp64: the same iterates to reordering."""
+    from deep_attention_visual_odometry_amd import _native
+
+    x = torch.tensor(x0, dtype=torch.float64, device=device)
+    compact = _solver(iterations=200, error_threshold=1e-12, minimum_step=1e-12)
+    out_c = compact(x, fn)
+    assert compact.last_generic_history is not None
+    with _native.debug_overrides(GENERIC_DENSE=1):
+        dense = _solver(iterations=200, error_threshold=1e-12, minimum_step=1e-12)
+        out_d = dense(x, fn)
+        assert dense.last_generic_history is None
+    assert torch.allclose(out_c, out_d, rtol=1e-8, atol=1e-10), (out_c, out_d)
+
+
+def test_calibration_network_closure_through_the_generic_loop(device):
+    """The reference caller's own closure (CalibrationNetwork's ray-angle error in torch) through the drop-in:
+    the compact generic loop against the oracle solve of the oracle's ray-angle closure (fp64, K = 10), and the
+    fp32 solve against the fused RayAngleError solve of the same problems."""
+    from deep_attention_visual_odometry_amd import BFGSSolver, RayAngleError, make_scenes
+    from deep_attention_visual_odometry_amd.geometry import calibration_network_error
+    from oracle import objective, solver
+
+    s = make_scenes(6, 2, 32, distortion=False, seed=77, ray_angle=True)
+    obs, vis, x0 = (torch.tensor(a) for a in (s.observations, s.visibility, s.initial))
+    kw = dict(iterations=10, error_threshold=-1.0, minimum_step=-1.0)
+    fn64 = calibration_network_error(obs.double().to(device), vis.double().to(device), 2, 32)
+    m = BFGSSolver(**kw).eval()
+    out = m(x0.double().to(device), fn64).cpu()
+    assert m.last_generic_history is not None
+    ref = solver.bfgs_solve(x0.double(), objective.RayAngleClosure(obs.double(), vis, 2, 32), **kw)
+    assert ((out - ref).norm(dim=-1) / ref.norm(dim=-1)).max().item() <= 1e-9
+    fn32 = calibration_network_error(obs.to(device), vis.float().to(device), 2, 32)
+    out32 = BFGSSolver(**kw).eval()(x0.to(device), fn32)
+    fused = BFGSSolver(**kw).eval()(x0.to(device), RayAngleError(obs.to(device), vis.to(device), 2, 32))
+    assert ((out32 - fused).double().norm(dim=-1) / fused.double().norm(dim=-1)).max().item() <= 1e-4
+
+
+def test_compact_generic_loop_memory_is_o_kp(device):
+    """C3's shape (P = 789) at B = 64, K = 30 through a closure: the compact rows grow with the iterations run
+    (O(k P) per problem), never to the dense (B, P, P) matrix (160 MB here)."""
+    from deep_attention_visual_odometry_amd import ReprojectionError, make_scenes
+
+    s = make_scenes(64, 4, 256, distortion=False, seed=3)
+    fn = ReprojectionError(torch.tensor(s.observations).to(device), torch.tensor(s.visibility).to(device), 4, 256)
+    x0 = torch.tensor(s.initial).to(device)
+    m = _solver(iterations=30, error_threshold=-1.0, minimum_step=-1.0)
+    m._generic(x0, fn, -1.0, 30)
+    hist = m.last_generic_history
+    assert hist is not None and hist.count == 29 and hist.capacity == 29
+    dense = 64 * 789 * 789 * 4
+    assert hist.nbytes() < dense / 6

@@ -16,11 +16,11 @@ CHILD = r"""
 import sys, numpy as np, torch
 sys.path[:0] = [%(repo)r, %(repo)r + "/deep-attention-visual-odometry_amd"]
 from deep_attention_visual_odometry_amd import make_scenes, native_ops
-s = make_scenes(%(batch)d, %(m)d, %(n)d, distortion=%(dist)r, seed=%(seed)d)
+s = make_scenes(%(batch)d, %(m)d, %(n)d, distortion=%(dist)r, seed=%(seed)d, ray_angle=%(ray)r)
 dev = torch.device("cuda", 0)
 x0, obs, vis = (torch.tensor(a, device=dev) for a in (s.initial, s.observations, s.visibility))
 x, _, st = native_ops.ba_solve(x0, obs, vis, %(m)d, %(n)d, %(dist)r, iterations=%(k)d, error_threshold=-1.0,
-                               minimum_step=-1.0, hessian_mode=%(mode)d, want_status=True)
+                               minimum_step=-1.0, hessian_mode=%(mode)d, want_status=True, residual=%(res)d)
 np.savez(%(out)r, x=x.cpu().numpy(), st=st.cpu().numpy())
 """
 
@@ -36,6 +36,7 @@ def main():
     ap.add_argument("--no-distortion", action="store_true")
     ap.add_argument("--k", type=int, default=100)
     ap.add_argument("--mode", type=int, default=1, help="0 = DENSE, 1 = COMPACT")
+    ap.add_argument("--residual", choices=["reprojection", "ray_angle"], default="reprojection")
     args = ap.parse_args()
     import numpy as np
 
@@ -44,7 +45,8 @@ def main():
     for tag, lib in (("a", args.lib_a), ("b", args.lib_b)):
         out = os.path.join(tmp, tag + ".npz")
         code = CHILD % dict(repo=REPO, batch=args.batch, m=args.views, n=args.points, dist=not args.no_distortion,
-                            seed=args.seed, k=args.k, out=out, mode=args.mode)
+                            seed=args.seed, k=args.k, out=out, mode=args.mode,
+                    ray=args.residual == "ray_angle", res=1 if args.residual == "ray_angle" else 0)
         subprocess.run([sys.executable, "-c", code], env=dict(os.environ, DAVA_DEBUG_OVERRIDES="1", DAVA_LIB=os.path.abspath(lib)),
                        check=True, timeout=300)
         res[tag] = np.load(out)

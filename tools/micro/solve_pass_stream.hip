@@ -6,6 +6,7 @@
 // same (non-zero) rows, so the two rates compare directly.  Prints GB/s of history rows read.
 // build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -fno-slp-vectorize -I../../include
 //        -I../../deep-attention-visual-odometry_amd/csrc solve_pass_stream.hip -o solve_pass_stream
+#define DAVA_DEVICE_PASSES_ONLY 1  // the device passes only, not the solve kernels and host API
 #include "../../deep-attention-visual-odometry_amd/csrc/bfgs_solve.hip"
 
 #include <cstdio>
