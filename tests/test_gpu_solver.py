@@ -383,6 +383,39 @@ def test_c5_reference_golden_trajectories(device, mode):
         assert ok, extra
 
 
+@pytest.mark.parametrize("mode", ["compact", "dense"])
+def test_c5_reference_golden_eight_problems(device, mode):
+    """The same comparison on the bench's first EIGHT C5 problems at K = 20 (tests/golden/c5_traj8.npz, made by
+    make_golden.py c5x8: the REAL reference from x0 and from x0 nudged one ulp up and down).  The scenes are
+    regenerated from the bench's seed; the fixture's x0 must match them bit for bit."""
+    from deep_attention_visual_odometry_amd import make_scenes
+
+    g = np.load(os.path.join(GOLDEN, "c5_traj8.npz"))
+    m, n = 16, 4096
+    s = make_scenes(8, m, n, distortion=False, seed=20251015 + 3000)
+    x0, obs, vis = torch.tensor(s.initial), torch.tensor(s.observations), torch.tensor(s.visibility)
+    assert np.array_equal(g["x0"], s.initial)
+    out, status = _gpu_solve(device, x0, obs, vis, m, n, False, iterations=20, error_threshold=-1.0,
+                             minimum_step=-1.0, hessian_mode=mode)
+    ref = torch.tensor(g["k20"])
+    assert (status[:, 0] == 20).all()
+    extra, ok = {}, True
+    for name, sl in {"whole": slice(None), **c5_blocks(m, n)}.items():
+        rel = _rel(out[:, sl], ref[:, sl])
+        spread = torch.maximum(_rel(torch.tensor(g["k20_up"])[:, sl], ref[:, sl]),
+                               _rel(torch.tensor(g["k20_down"])[:, sl], ref[:, sl]))
+        env = torch.clamp(ENVELOPE_FACTOR * spread, min=TOL)
+        extra[f"{name}_max_rel"] = float(rel.max())
+        extra[f"{name}_spread_1ulp_max"] = float(spread.max())
+        extra[f"{name}_max_rel_over_1ulp"] = float((rel / spread.clamp(min=1e-300)).max())
+        extra[f"{name}_n_outside_envelope"] = int((rel > env).sum())
+        ok &= bool((rel <= env).all())
+    rel = _rel(out, ref)
+    _report(f"golden_c5x8_{mode}_K20", rel, None, extra)
+    assert (rel <= TOL).all(), rel
+    assert ok, extra
+
+
 @pytest.mark.parametrize("xl", [True, False])
 def test_global_vector_packed_sweep_ragged_points_match_oracle(device, xl, overrides):
     """GV mode's packed pair sweep (two of a thread's points per step) with a ragged point count

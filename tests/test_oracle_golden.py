@@ -364,3 +364,17 @@ def test_c5_trajectory_matches_reference_bitwise():
     out = solver.bfgs_solve(x0, objective.ReprojectionClosure(obs, vis, 16, 4096), iterations=20,
                             error_threshold=-1.0, minimum_step=-1.0)
     assert np.array_equal(out.numpy(), g["k20"])
+
+
+def test_c5_eight_problem_fixture_extends_the_pinned_one():
+    """tests/golden/c5_traj8.npz (the real reference at K = 20 on the bench's first EIGHT C5 problems, with its
+    1-ulp-nudged runs) starts with the two problems of c5_traj.npz, which the oracle reproduces bit for bit
+    (test above): the same x0 rows and the same reference results there, so the eight-problem fixture comes
+    from the same algorithm."""
+    g2 = np.load(os.path.join(GOLDEN, "c5_traj.npz"))
+    g8 = np.load(os.path.join(GOLDEN, "c5_traj8.npz"))
+    assert g8["x0"].shape == (8, 12381) and g8["k20"].shape == (8, 12381)
+    assert np.array_equal(g8["x0"][:2], g2["x0"])
+    for key in ("k20", "k20_up", "k20_down"):
+        assert np.array_equal(g8[key][:2], g2[key]), key
+        assert np.isfinite(g8[key]).all()
