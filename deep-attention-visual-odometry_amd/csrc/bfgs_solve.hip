@@ -1561,6 +1561,20 @@ __global__ __launch_bounds__(kWave * NW, kSolveWavesPerEU) void bfgs_ba_solve_ke
       }
       const float alpha = a_hi;
       if (a.tape_s && tid == 0) a.tape_s[(size_t)b * a.tape_T + k] = alpha;
+      if constexpr (kLeanTrials && !kTrialDot) {
+        if (evaluated && last_al == alpha && !last_same && !last_grad) {  // uniform
+          // The accepted trial was lean: evaluate it again in the full trial form (the same point, formed
+          // the same way, the same instantiation as a first trial), so x_{k+1}'s objective and gradient are
+          // bit for bit those the full-trial path keeps -- the trajectory does not depend on which trial of
+          // the search was accepted.  Rejected trials (the zoom tails of C2's slowest problems) stay lean.
+          float f2, s2;
+          ba_eval<true, !kTrialDot, true, kTrialDot, true, RES, float, NW, PPT, GV>(
+              L, x, d, alpha, obs, vis, grad_buf(gp), views, vpart, scratch, buf, f2, s2);
+          ++evals;
+          last_fa = f2;
+          last_grad = true;
+        }
+      }
       have_next = evaluated && last_al == alpha && (last_same || last_grad);
       E_next = last_fa;
       if (have_next && last_same) {  // x_{k+1} == x_k bitwise: its gradient is g itself
