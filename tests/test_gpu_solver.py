@@ -21,13 +21,21 @@ from oracle import objective, solver
 pytestmark = pytest.mark.gpu
 
 TOL = 1e-5
-# Per-block envelopes: this many times the reference's own change under a 1-ulp nudge of x0 (floor TOL).
-# 5: the largest ratios measured past the 1e-5 floor are 4.12 (the headline's problem 13 run to the
-# reference's stopping rules, distortion block, test_headline_converged_parameters_match_oracle),
-# 3.65 (C5, dense, extrinsics block at K = 100, profiles/r05_c5_parity_distribution.jsonl) and 3.03 (the
-# headline's problem 39 at K = 100, distortion block, profiles/r05_trace_intrinsics.jsonl; DESIGN 4.3
-# traces where they come from).  Rounds 1-4 used 10.
-ENVELOPE_FACTOR = 5.0
+
+
+def _envelope_factor():
+    """Per-block envelopes: this many times the reference's own change under a 1-ulp nudge of x0 (floor TOL).
+    Derived from the oracle alone (tests/golden/make_envelope.py -> parity_envelope.json, re-derived and checked
+    by tests/test_parity_envelope.py): the smallest factor whose envelope holds the oracle's own spread when
+    every evaluation it sees carries last-bit noise -- what a reordered fp32 sum does.  No GPU result enters it.
+    (r05 used 5, the smallest integer above the largest GPU ratio then measured, 4.12.)"""
+    import json
+
+    with open(os.path.join(GOLDEN, "parity_envelope.json")) as fh:
+        return float(json.load(fh)["envelope_factor"])
+
+
+ENVELOPE_FACTOR = _envelope_factor()
 
 
 def _scene(b, m, n, distortion, seed):

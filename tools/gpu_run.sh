@@ -12,6 +12,8 @@
 #   micro=P               tools/micro/solve_pass_stream P (the history pass alone; P > 512: the headline's rows)
 #   eval=TAG              tools/eval_sweep.py (C3, C5) + tools/profile_eval.sh TAG for both
 #   ab=SPEC;SPEC...       tools/ab_env.sh with the given specs (BENCH_ARGS from the environment)
+#   phase                 tools/phase_scan.sh (needs build/var_phase: make variant NAME=phase FLAGS=-DDAVA_PHASE_TIMING=1)
+#   closure               tools/closure_scan.sh (bench --entry closure: compact vs dense generic loop, C2 and C3)
 # usage: tools/gpu_run.sh tests smoke bench profile=r02a
 set -uo pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -74,6 +76,14 @@ for s in "$@"; do
       tag=${val%%:*}; args=${val#*:}; [ "$args" = "$val" ] && args=""
       tools/pmc_sq.sh "$tag" $args > gpurun_out/sq_$tag.log 2>&1 || { tail -5 gpurun_out/sq_$tag.log; exit 1; }
       tail -3 gpurun_out/sq_$tag.log ;;
+    phase)
+      step phase
+      tools/phase_scan.sh > gpurun_out/phase_scan.log 2>&1 || { tail -5 gpurun_out/phase_scan.log; exit 1; }
+      cut -c1-300 gpurun_out/phase_scan.log ;;
+    closure)
+      step closure "$val"
+      tools/closure_scan.sh > gpurun_out/closure.jsonl 2> gpurun_out/closure.err || { tail -5 gpurun_out/closure.err; exit 1; }
+      cut -c1-400 gpurun_out/closure.jsonl ;;
     ab)
       step ab "$val"
       IFS=';' read -ra specs <<< "$val"
