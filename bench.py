@@ -229,7 +229,9 @@ def cpu_baseline(args, x0, obs, vis, x_gpu):
         parity["over_per_evaluation_ulp_noise"] = {
             k: {"max": float((r[:m] / noise[key].clamp(min=1e-300)).max()),
                 "median": float((r[:m] / noise[key].clamp(min=1e-300)).median()),
-                "spread_max": float(noise[key].max())}
+                "spread_max": float(noise[key][torch.isfinite(noise[key])].max()) if torch.isfinite(noise[key]).any()
+                else None,
+                "n_noise_runs_nonfinite": int((~torch.isfinite(noise[key])).sum())}
             for k, key, r in (("whole", "x", rel), ("intrinsics", "i", rel_i),
                               ("distortion", "d", _rel(gpu[:, -5:], ref[:, -5:])))}
         parity["over_per_evaluation_ulp_noise"]["note"] = (
@@ -285,7 +287,10 @@ def ulp_noise_spread(solver, x0, closure, kw, ref, seeds=(1, 2)):
     for seed in seeds:
         noisy = solver.bfgs_solve(x0, closure, ulp_noise=torch.Generator().manual_seed(seed), **kw)
         for key, sl in BLOCKS:
-            out[key] = torch.maximum(out[key], _rel(noisy[:, sl], ref[:, sl]))
+            r = _rel(noisy[:, sl], ref[:, sl])
+            # a noisy run that walks to inf / NaN (a wild trial under Brown-Conrady): an unbounded spread, so that
+            # problem drops out of the ratios (GPU distance / inf = 0) instead of turning them into NaN
+            out[key] = torch.maximum(out[key], torch.where(torch.isfinite(r), r, torch.full_like(r, float("inf"))))
     return out
 
 
@@ -328,7 +333,10 @@ def converged_parity(args, x0, obs, vis, closure, n_env, dev):
         blocks[name] = {"max_rel": float(r.max()), "frac_le_1e-5": float((r <= PARITY_BAR).double().mean()),
                         "over_1ulp_nudge_max": float((r[:m] / spread[key].clamp(min=1e-300)).max()),
                         "over_ulp_noise_max": float((r[:m] / noise[key].clamp(min=1e-300)).max()),
-                        "nudge_spread_max": float(spread[key].max()), "noise_spread_max": float(noise[key].max())}
+                        "nudge_spread_max": float(spread[key].max()),
+                        "noise_spread_max": float(noise[key][torch.isfinite(noise[key])].max())
+                        if torch.isfinite(noise[key]).any() else None,
+                        "n_noise_runs_nonfinite": int((~torch.isfinite(noise[key])).sum())}
     return {"n": n, "rules": "error_threshold 1e-4, iterations 1000, minimum_step 1e-8 (bfgs_solver.py:53-55)",
             "per_parameter": per, "blocks": blocks, "envelope_problems": m,
             "same_stop_iteration": float((st[:16, 0] == rec.iterations.to(st.dtype)).double().mean()),

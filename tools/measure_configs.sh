@@ -19,4 +19,10 @@ run C3 --steps 3 &&
 run C3_pinhole --no-distortion &&
 run C3_ray --no-distortion --residual ray_angle &&
 run C3_dense --mode dense --steps 1 &&
-run C5 --batch 256 --views 16 --points 4096 --no-distortion --steps 1
+run C5 --batch 256 --views 16 --points 4096 --no-distortion --steps 1 || exit 1
+# solve + gradient (the recording solve and the fused adjoint), C2 / C3 / C5 (DIFF=0 skips them)
+if [ "${DIFF:-1}" = 1 ]; then
+  run C2_grad --batch 1024 --views 2 --points 128 --no-distortion --differentiate &&
+  run C3_grad --differentiate --steps 2 &&
+  run C5_grad --batch 256 --views 16 --points 4096 --no-distortion --differentiate --steps 1
+fi

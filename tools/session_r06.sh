@@ -1,22 +1,24 @@
 #!/bin/bash
-# Round-6 GPU session (repo root on the box): the in-tree build against the r05 build and a variant.
-#   1. bitwise: r05 vs the in-tree build at C2, C3 (B = 2048), C2 ray-angle and C5 (B = 64), full solves row by row
-#   2. interleaved timing: r05 / VARIANT / in-tree at C2, C2 ray-angle, C3 and C5
-# usage: tools/session_r06.sh [VARIANT_NAME]   (build/var_VARIANT_NAME; default novl)
+# Round-6 GPU session (repo root on the box).
+#   lean : interleaved timing of the first lean trial index (in-tree = 1, build/var_lean2, build/var_lean3)
+#          at C2, C2 ray-angle and C3, after a bitwise check of each against the in-tree build
+#   diag : tools/eval_bitwise.py (the objective's trial forms, bit for bit), phase cycles (build/var_phase)
+#          and the closure entry (compact vs dense generic loop)
+# usage: tools/session_r06.sh lean|diag ...
 set -uo pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$R"
 mkdir -p gpurun_out
-V=${1:-novl}
-B=deep-attention-visual-odometry_amd/build
-LIB=deep-attention-visual-odometry_amd/deep_attention_visual_odometry_amd/_lib/libdava_ba.so
-for c in "--batch 1024 --views 2 --points 128 --no-distortion" "--batch 2048" \
-         "--batch 1024 --views 2 --points 128 --no-distortion --residual ray_angle" \
-         "--batch 64 --views 16 --points 4096 --no-distortion"; do
-  echo "== bitwise r05 vs new: $c"
-  timeout -k 10 300 python3 tools/lib_compare.py $B/var_r05/libdava_ba.so $LIB --seed 20254015 $c 2>&1 | grep -v amdgpu.ids | head -6 || exit 1
+for s in "$@"; do
+  case $s in
+    lean)
+      tools/ab.sh -r 2 -c "C2:--batch 1024 --views 2 --points 128 --no-distortion" \
+        -c "C2_ray:--batch 1024 --views 2 --points 128 --no-distortion --residual ray_angle" -c "C3:" \
+        "lean1:" "lean2:DAVA_LIB=@BUILD@/var_lean2/libdava_ba.so" "lean3:DAVA_LIB=@BUILD@/var_lean3/libdava_ba.so" \
+        2>&1 | cut -c1-260 || exit 1 ;;
+    diag)
+      echo "== eval_bitwise"
+      timeout -k 10 300 python3 tools/eval_bitwise.py 2>&1 | grep -v amdgpu.ids || exit 1
+      tools/gpu_run.sh phase closure || exit 1 ;;
+  esac
 done
-tools/ab.sh -r 2 -c "C2:--batch 1024 --views 2 --points 128 --no-distortion" \
-  -c "C2_ray:--batch 1024 --views 2 --points 128 --no-distortion --residual ray_angle" -c "C3:" \
-  -c "C5:--batch 256 --views 16 --points 4096 --no-distortion --steps 1" \
-  "r05:DAVA_LIB=@BUILD@/var_r05/libdava_ba.so" "$V:DAVA_LIB=@BUILD@/var_$V/libdava_ba.so" "new:" 2>&1 | cut -c1-260
