@@ -175,23 +175,34 @@ __device__ __forceinline__ void st4(float* p, float4 v) { *reinterpret_cast<floa
 // boxes, not kept.)
 constexpr int kFusedBufferLoadsGM = 2;
 constexpr int kSweepRows = 4;  // DENSE sweep: matrix rows in flight per lane
-// Trial slopes phi'(alpha): forward mode (a JVP riding on the trial's evaluation) in LDS mode, where
-// the reverse-mode form d . grad measured -1% at C3 (profiles/r01b_ab_variants.log, `dot`); d . grad in
-// global-vector mode, where it saves the pair sweep's tangent registers (C5 +4%, r03 interleaved A/B).
-constexpr bool kTrialDotLds = false;
-constexpr bool kTrialDotGv = true;
-// Lean trials (LDS mode, r06): only a line search's first trial forms the reverse-mode gradient.  Every
-// later trial (widening or zoom) is evaluated for E and the forward-mode slope alone -- all the Wolfe tests
-// read (wolfe_conditions.py:116-237) -- and, if it is the one accepted, the next iteration evaluates the
-// gradient at x_{k+1} instead of reusing the trial's.  The alpha sequence is bitwise unchanged (the same E
-// and slope arithmetic, reduced in the same order).  GV mode keeps its reverse-mode trial slope (d . grad,
-// kTrialDotGv), whose rounding the forward-mode slope would not reproduce.
-// DAVA_LEAN_TRIALS: the first trial index evaluated lean (0: none).
-#ifndef DAVA_LEAN_TRIALS
-#define DAVA_LEAN_TRIALS 1
+// Trial slopes phi'(alpha) of the full trials (the ones that also form the gradient): forward mode (a JVP
+// riding on the trial's evaluation) in LDS mode, where the reverse-mode form d . grad measured -1% at C3
+// (profiles/r01b_ab_variants.log, `dot`); d . grad in global-vector mode, where it saves the pair sweep's
+// tangent registers (C5 +4%, r03 interleaved A/B).  DAVA_TRIAL_DOT_LDS=1: d . grad in LDS mode too (A/B).
+#ifndef DAVA_TRIAL_DOT_LDS
+#define DAVA_TRIAL_DOT_LDS 0
 #endif
-constexpr int kLeanFrom = DAVA_LEAN_TRIALS;
-constexpr bool kLeanTrials = kLeanFrom > 0;
+constexpr bool kTrialDotLds = DAVA_TRIAL_DOT_LDS != 0;
+constexpr bool kTrialDotGv = true;
+// Lean trials (r06): a line search's trials from index kLeanFrom on are evaluated for E and the forward-mode
+// slope alone -- all the Wolfe tests read (wolfe_conditions.py:116-237) -- without the reverse-mode gradient.
+// If the accepted trial was lean, it is evaluated once more in the full trial form (below), so x_{k+1}'s
+// objective and gradient are bit for bit what the full-trial path keeps.  The first trials (alpha = 1, accepted
+// ~89% of the time at C3) stay full.  DAVA_LEAN_TRIALS (LDS mode) / DAVA_LEAN_TRIALS_GV: the first trial index
+// evaluated lean, 0 = none.  LDS mode from the third trial: a search of two trials (reject, accept) would pay
+// the lean trial and its full re-evaluation; interleaved A/B (profiles/r06f_lean_index_dot_gvlean_ab.log):
+// from the 2nd / 3rd / 4th trial C2 0.514 / 0.514 / 0.505, C2 ray-angle 0.683 / 0.691 / 0.695, C3 0.895 for all
+// (no lean trials: C2 0.46).  GV mode keeps full trials: lean from the 2nd / 3rd trial C5 -1.5% / -1.2% (its
+// searches are short, and a lean trial's forward-mode tangents cost the packed sweep registers).  First
+// trials with d . grad in LDS mode too (DAVA_TRIAL_DOT_LDS=1): C3 -1.1%, C2 -0.5%, not kept.
+#ifndef DAVA_LEAN_TRIALS
+#define DAVA_LEAN_TRIALS 2
+#endif
+#ifndef DAVA_LEAN_TRIALS_GV
+#define DAVA_LEAN_TRIALS_GV 0
+#endif
+constexpr int kLeanFromLds = DAVA_LEAN_TRIALS;
+constexpr int kLeanFromGv = DAVA_LEAN_TRIALS_GV;
 // Runs of known no-move zoom trials iterated as the scalar recurrence they are (r06; bitwise invisible).
 #ifndef DAVA_NOMOVE_RUNS
 #define DAVA_NOMOVE_RUNS 1
@@ -1122,6 +1133,8 @@ __global__ __launch_bounds__(kWave * NW, kSolveWavesPerEU) void bfgs_ba_solve_ke
   static_assert(GV ? NW == solve_waves(true) : (NW == 1 || NW == 2 || NW == 4), "LDS mode runs 1-, 2- or 4-wave workgroups");
   constexpr int BLOCK = kWave * NW;
   constexpr bool kTrialDot = GV ? kTrialDotGv : kTrialDotLds;
+  constexpr int kLeanFrom = GV ? kLeanFromGv : kLeanFromLds;
+  constexpr bool kLean = kLeanFrom > 0;
   extern __shared__ __attribute__((aligned(16))) float lds[];
   __builtin_amdgcn_s_setprio(kBasePrio);
   const Layout L = a.L;
@@ -1458,7 +1471,7 @@ __global__ __launch_bounds__(kWave * NW, kSolveWavesPerEU) void bfgs_ba_solve_ke
         // phi'(0).  The check rides on the objective's first reduction (CHECK).  Otherwise
         // E and the full gradient at the trial point are formed (kept for reuse as the
         // next iterate's gradient) and phi'(alpha) = d . grad (DOT) -- for the first trial;
-        // later ones form E and phi'(alpha) only (kLeanTrials).
+        // later ones form E and phi'(alpha) only (kLean).
         const bool known_same = al <= nomove_al;  // uniform
         if (kNoMoveRuns && known_same && zoom && E >= f_lo) {
           // A run of known no-move trials in the zoom phase: each trial point is x itself (f = E, phi' =
@@ -1485,7 +1498,6 @@ __global__ __launch_bounds__(kWave * NW, kSolveWavesPerEU) void bfgs_ba_solve_ke
           dfa = dphi0;
           continue;
         }
-        constexpr bool kLean = kLeanTrials && !kTrialDot;
         const bool lean = kLean && t >= kLeanFrom;  // uniform
         bool moved = false;
         if (!known_same) {
@@ -1501,10 +1513,9 @@ __global__ __launch_bounds__(kWave * NW, kSolveWavesPerEU) void bfgs_ba_solve_ke
           last_same = false;
           last_grad = !lean;
           if (kLean && lean && !(isfinite(fa) && isfinite(dfa))) {
-            // overflowed lean trial: the rule below needs the reverse-mode gradient (rare; the same point,
-            // so the same E)
-            ba_eval<true, true, true, false, false, RES, float, NW, PPT, GV>(L, x, d, al, obs, vis, grad_buf(gp), views,
-                                                                      vpart, scratch, buf, fa, dfa);
+            // overflowed lean trial: the rule below needs the reverse-mode gradient (rare): the full trial form
+            ba_eval<true, !kTrialDot, true, kTrialDot, false, RES, float, NW, PPT, GV>(
+                L, x, d, al, obs, vis, grad_buf(gp), views, vpart, scratch, buf, fa, dfa);
             ++evals;
             last_grad = true;
           }
@@ -1561,7 +1572,7 @@ __global__ __launch_bounds__(kWave * NW, kSolveWavesPerEU) void bfgs_ba_solve_ke
       }
       const float alpha = a_hi;
       if (a.tape_s && tid == 0) a.tape_s[(size_t)b * a.tape_T + k] = alpha;
-      if constexpr (kLeanTrials && !kTrialDot) {
+      if constexpr (kLean) {
         if (evaluated && last_al == alpha && !last_same && !last_grad) {  // uniform
           // The accepted trial was lean: evaluate it again in the full trial form (the same point, formed
           // the same way, the same instantiation as a first trial), so x_{k+1}'s objective and gradient are

@@ -245,15 +245,29 @@ class BFGSSolver(Module):
         return _native.DAVA_HESSIAN_COMPACT
 
     def _generic(self, parameters, error_function, error_threshold, num_iterations):
+        """The reference's loop (bfgs_solver.py:94-212) around any closure: closure + autograd in torch, every
+        solver op a HIP kernel.  The active set is gathered and scattered by index (the rows of `updating`, taken
+        once per use of a new active set) instead of by the reference's boolean masks: the same rows and values
+        in the same order, but one host round trip where every boolean gather or masked_scatter takes one."""
         batch_dimensions = parameters.shape[:-1]
         parameter_dim = parameters.size(-1)
         device = parameters.device
         updating = torch.ones(batch_dimensions, dtype=torch.bool, device=device)
+        n_total = updating.numel()
+        rows = torch.arange(n_total, device=device)  # flat indices of the active problems, batch order
+        rows_box = [rows]  # the closure wrapper's view of the current active rows
 
         def wrapped(inner_parameters: torch.Tensor, inner_mask: torch.Tensor) -> torch.Tensor:
-            mask = torch.zeros_like(updating)
-            mask[updating] = inner_mask
-            return error_function(inner_parameters, mask)
+            mask = torch.zeros((n_total,), dtype=torch.bool, device=device)
+            mask[rows_box[0]] = inner_mask.reshape(-1)  # (index put: no host sync)
+            return error_function(inner_parameters, mask.reshape(batch_dimensions))
+
+        def take(t: torch.Tensor, idx: torch.Tensor) -> torch.Tensor:  # t[updating], flattened as the reference's
+            return t.reshape((n_total,) + t.shape[len(batch_dimensions):]).index_select(0, idx)
+
+        def put(t: torch.Tensor, idx: torch.Tensor, v: torch.Tensor) -> torch.Tensor:  # t.masked_scatter(updating, v)
+            flat = t.reshape((n_total,) + t.shape[len(batch_dimensions):])
+            return flat.index_copy(0, idx, v.reshape((idx.numel(),) + flat.shape[1:])).reshape(t.shape)
 
         create_graph = parameters.requires_grad  # bfgs_solver.py:85
         if not create_graph:
@@ -268,8 +282,7 @@ class BFGSSolver(Module):
         if (not create_graph and device.type == "cuda" and self.hessian_mode != "dense"
                 and not _native.python_knob("GENERIC_DENSE")
                 and native_ops.CompactHistory.supported(parameter_dim, parameters.dtype, num_iterations - 1)):
-            n_problems = max(int(torch.tensor(batch_dimensions).prod().item()) if len(batch_dimensions) else 1, 1)
-            history = native_ops.CompactHistory(n_problems, parameter_dim, parameters.dtype, device,
+            history = native_ops.CompactHistory(max(n_total, 1), parameter_dim, parameters.dtype, device,
                                                 max_entries=num_iterations - 1)
             inverse_hessian = None
         else:
@@ -281,47 +294,52 @@ class BFGSSolver(Module):
             prev_gradient = gradient
             if self.training and self.drop_path_p > 0.0:
                 updating = updating & torch.greater(torch.rand_like(updating, dtype=torch.float32), self.drop_path_p)
-            upd_params = parameters[updating]
+                rows = updating.reshape(-1).nonzero().squeeze(1)
+            rows_box[0] = rows
+            upd_params = take(parameters, rows)
             if not upd_params.requires_grad:
                 upd_params.requires_grad_(True)
             with torch.enable_grad():
                 upd_error = error_function(upd_params, updating)
                 (upd_grad,) = torch.autograd.grad(upd_error.sum(), upd_params, create_graph=create_graph)
-            error = error.masked_scatter(updating, upd_error.detach())
-            gradient = gradient.masked_scatter(updating.unsqueeze(-1).expand_as(gradient), upd_grad)
+            error = put(error, rows, upd_error.detach())
+            gradient = put(gradient, rows, upd_grad)
             updating = updating & torch.greater(error, error_threshold)
-            if not bool(torch.any(updating)):
+            rows = updating.reshape(-1).nonzero().squeeze(1)
+            if rows.numel() == 0:
                 break
-            upd_params = parameters[updating]
-            upd_error = error[updating]
-            upd_grad = gradient[updating]
+            rows_box[0] = rows
+            upd_params = take(parameters, rows)
+            upd_error = take(error, rows)
+            upd_grad = take(gradient, rows)
             if step_idx == 0:
                 direction = -1.0 * upd_grad
             elif history is not None:
-                active = torch.nonzero(updating.reshape(-1)).squeeze(1)  # flat problem indices, batch order
-                direction = history.direction(upd_grad, upd_grad - prev_gradient[updating], step[updating],
-                                              active).reshape(upd_grad.shape)
+                direction = history.direction(upd_grad, upd_grad - take(prev_gradient, rows), take(step, rows),
+                                              rows).reshape(upd_grad.shape)
             else:
-                delta = upd_grad - prev_gradient[updating]
-                upd_h = inverse_hessian[updating]
-                upd_step = step[updating]
+                delta = upd_grad - take(prev_gradient, rows)
+                upd_h = take(inverse_hessian, rows)
+                upd_step = take(step, rows)
                 if step_idx == 1:
                     upd_h = native_ops.scale_matrix(native_ops.initial_scale(upd_step, delta), upd_h)
                 upd_h = native_ops.update_inverse_hessian(upd_h, upd_step, delta)
                 direction = native_ops.search_direction(upd_h, upd_grad)
-                inverse_hessian = inverse_hessian.masked_scatter(
-                    updating.unsqueeze(-1).unsqueeze(-1).expand_as(inverse_hessian), upd_h)
+                inverse_hessian = put(inverse_hessian, rows, upd_h)
             step_size = line_search_wolfe_conditions(
                 upd_params, direction, upd_error, upd_grad, wrapped,
                 sufficient_decrease=self.sufficient_decrease, curvature=self.curvature, strong=True)
             upd_step = step_size.unsqueeze(-1) * direction
             new_params = upd_params + upd_step
-            step = step.masked_scatter(updating.unsqueeze(-1).expand_as(step), upd_step)
+            step = put(step, rows, upd_step)
             if not self.training or not self.return_second_last:
-                parameters = parameters.masked_scatter(updating.unsqueeze(-1).expand_as(parameters), new_params)
+                parameters = put(parameters, rows, new_params)
             updating = updating & torch.greater(torch.linalg.vector_norm(step, dim=-1), self.minimum_step)
-            if not bool(torch.any(updating)):
+            rows = updating.reshape(-1).nonzero().squeeze(1)
+            if rows.numel() == 0:
                 break
             if self.training and self.return_second_last:
-                parameters = parameters.masked_scatter(updating.unsqueeze(-1).expand_as(parameters), new_params)
+                # the reference scatters the previous active set's new parameters into the smaller new active set
+                # (bfgs_solver.py:208-212): masked_scatter takes new_params' leading rows, in order
+                parameters = put(parameters, rows, new_params[: rows.numel()])
         return parameters if create_graph else parameters.detach()

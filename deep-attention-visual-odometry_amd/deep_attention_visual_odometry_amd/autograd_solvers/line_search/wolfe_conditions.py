@@ -7,8 +7,9 @@ trials, result = the upper bracket) runs in HIP kernels
 (``dava_wolfe_{init,propose,update}``; on CPU tensors the library's host flavours
 ``dava_cpu_wolfe_*``); only the caller's ``error_function`` and its derivative w.r.t.
 alpha are evaluated by PyTorch, where the tensors live.
-The host loop still asks "is any problem active?" once per trial, exactly
-where the reference synchronises (``wolfe_conditions.py:119-121``).
+The host loop still asks "which problems are active?" once per trial, exactly
+where the reference synchronises (``wolfe_conditions.py:119-121``), and gathers
+the active rows by index (no further host round trips of its own).
 
 The fused BA solver does not use this function: it runs the same state
 machine inside its persistent kernel with no host round-trips.
@@ -47,18 +48,24 @@ def line_search_wolfe_conditions(
     batch_shape = parameters.shape[:-1]
 
     state = WolfeState(search_direction, base_error, base_gradient)
+    flat_parameters = parameters.reshape(-1, parameters.shape[-1])
+    flat_direction = search_direction.reshape(-1, search_direction.shape[-1])
     for trial in range(1000):
         active = state.active()
-        if not bool(active.any()):  # host sync, as in the reference
+        # the active rows, once: the trial's only host sync besides the closure's own (where the reference
+        # synchronises, wolfe_conditions.py:119-121); the gathers below index with them instead of the boolean
+        # mask, whose every use is another nonzero() and host round trip -- the same rows, the same values
+        rows = active.nonzero().squeeze(-1)
+        if rows.numel() == 0:
             break
         if trial > 0:
             state.propose()
         mask = active.reshape(batch_shape)
-        alpha = state.state[active, WolfeState.A].clone().unsqueeze(-1).requires_grad_(True)
+        alpha = state.state.index_select(0, rows)[:, WolfeState.A].clone().unsqueeze(-1).requires_grad_(True)
         with torch.enable_grad():
-            err = error_function(parameters[mask] + alpha * search_direction[mask], mask)
+            err = error_function(flat_parameters.index_select(0, rows) + alpha * flat_direction.index_select(0, rows),
+                                 mask)
             (slope,) = torch.autograd.grad(err.sum(), alpha)
-        rows = active.nonzero().squeeze(-1)
         state.state[rows, WolfeState.F_A] = err.detach().reshape(-1).to(state.state.dtype)
         state.state[rows, WolfeState.DPHI_A] = slope.detach().reshape(-1).to(state.state.dtype)
         state.update(trial, sufficient_decrease, curvature, strong)
