@@ -101,9 +101,17 @@ class BFGSSolver(Module):
     # ---- forward ----
     def forward(self, parameters: torch.Tensor,
                 error_function: Callable[[torch.Tensor, torch.Tensor], torch.Tensor]) -> torch.Tensor:
-        if isinstance(error_function, ReprojectionError) or not isinstance(parameters, torch.Tensor) \
-                or parameters.device.type != "cpu":
-            _native.require_device_tensor(parameters, "parameters")  # the fused objectives are GPU-only
+        if not isinstance(parameters, torch.Tensor) or parameters.device.type != "cpu":
+            _native.require_device_tensor(parameters, "parameters")
+        if isinstance(error_function, ReprojectionError) and parameters.device.type == "cpu":
+            # CPU tensors: the fused objectives are GPU kernels, so the generic loop runs on the library's host
+            # flavours with the objective's torch form (ReprojectionError on CPU tensors), as the reference solves
+            # wherever the parameters live (bfgs_solver.py:94-117)
+            self.last_status = None
+            if self.training:
+                return self._generic(parameters, error_function, self.training_error_threshold,
+                                     self.training_iterations)
+            return self._generic(parameters, error_function, self.error_threshold, self.iterations)
         if self.training:
             error_threshold, num_iterations = self.training_error_threshold, self.training_iterations
         else:

@@ -129,7 +129,8 @@ class ReprojectionError:
             raise ValueError("visibility must have shape observations.shape[:-1]")
         if num_views < 2:
             raise ValueError("num_views must be >= 2")
-        self.observations = observations.to(torch.float32)
+        # (device tensors: the kernels read float32; CPU tensors keep their dtype for the torch objective)
+        self.observations = observations if observations.device.type == "cpu" else observations.to(torch.float32)
         self.visibility = visibility.to(torch.uint8)
         self.num_views = int(num_views)
         self.num_points = int(num_points)
@@ -154,10 +155,21 @@ class ReprojectionError:
         x = parameters.reshape(-1, parameters.size(-1))
         obs = obs.reshape(-1, self.num_views, self.num_points, 2)
         vis = vis.reshape(-1, self.num_views, self.num_points)
+        if x.device.type == "cpu":
+            # CPU tensors: the same objective as torch ops (geometry.closure_ops), so the drop-in solves where
+            # the parameters live, as the reference does (bfgs_solver.py:94-117); autograd gives its derivatives
+            # to any order.  Device tensors take the HIP kernels below, never this.
+            return self._torch_objective(x, obs.to(x.dtype), vis).reshape(lead)
         if x.dtype != torch.float32:
             raise TypeError("ReprojectionError evaluates in float32")
         err = _NativeObjective.apply(x, obs, vis, self.num_views, self.num_points, self.distortion, self.residual)
         return err.reshape(lead)
+
+
+    def _torch_objective(self, x, obs, vis):
+        from ..geometry.closure_ops import reprojection_objective
+
+        return reprojection_objective(x, obs, vis, self.num_views, self.num_points, self.distortion)
 
 
 class RayAngleError(ReprojectionError):
@@ -170,13 +182,18 @@ class RayAngleError(ReprojectionError):
     camera-relative point (``camera_model/calibration_pinhole_camera_model.py:78-117``)
     and the angle in Kahan's form 2 atan2(|a^ - b^|, |a^ + b^|)
     (``geometry/projective_plane_angle_distance.py:20-64``).  Pinhole parameter
-    layout only; the fused solver and the evaluation kernel both run it on the GPU.
+    layout only; the fused solver and the evaluation kernel both run it on the GPU (on CPU tensors, torch ops).
     """
 
     residual = native_ops.N.DAVA_RESIDUAL_RAY_ANGLE
 
     def __init__(self, observations: torch.Tensor, visibility: torch.Tensor, num_views: int, num_points: int):
         super().__init__(observations, visibility, num_views, num_points, distortion=False)
+
+    def _torch_objective(self, x, obs, vis):
+        from ..geometry.closure_ops import ray_angle_objective
+
+        return ray_angle_objective(x, obs, vis, self.num_views, self.num_points)
 
 
 from .pinhole_camera_model_l1 import PinholeCameraModelL1  # noqa: E402  (legacy IOptimisableFunction model)

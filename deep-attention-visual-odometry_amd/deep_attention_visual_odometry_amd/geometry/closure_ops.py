@@ -15,7 +15,13 @@ closure is the caller's, not the hot path (the fused kernels evaluate the same o
     2 atan2(|a^ - b^|, |a^ + b^|), norms clamped at 2^-52);
   * ``get_camera_relative_points``: ``camera_model/calibration_pinhole_camera_model.py:78-117``, with the
     scale means kept as (B, 1, 1, 1) so that it broadcasts for B > 1 (the reference's means drop those
-    dimensions, which breaks any batch other than 1).
+    dimensions, which breaks any batch other than 1; SURVEY.md 0.5);
+  * ``project_points_basic_pinhole``: ``geometry/camera_projection.py:20-35`` (f xy / z + c);
+  * ``project_points_brown_conrady``: ``camera_model/distorted_camera_model.py:24-103`` at the BA
+    objective's camera (fx = fy = f, skew 0, the extrinsics already applied): the z' == 0 nudge, the
+    f-scaled coordinates and the radial / tangential block, in the reference's operation order.
+``reprojection_objective`` / ``ray_angle_objective`` compose them into the objectives the fused kernels
+evaluate (``ReprojectionError`` / ``RayAngleError`` on CPU tensors run these; on the GPU the kernels).
 """
 import torch
 from torch.nn.functional import elu
@@ -159,3 +165,59 @@ def calibration_network_error(true_projected_points: torch.Tensor, visibility_ma
         return (distance * visibility_mask[batch_mask]).sum(dim=(-1, -2))
 
     return error_function
+
+
+def project_points_basic_pinhole(points: torch.Tensor, intrinsics: torch.Tensor) -> torch.Tensor:
+    """(B..., 3) camera-relative points and (B..., 3) intrinsics (f, cx, cy) -> (B..., 2) pixels."""
+    return intrinsics[..., 0:1] * points[..., 0:2] / points[..., 2:3] + intrinsics[..., 1:3]
+
+
+def project_points_brown_conrady(points: torch.Tensor, intrinsics: torch.Tensor,
+                                 coefficients: torch.Tensor) -> torch.Tensor:
+    """(B..., 3) camera-relative points, (B..., 3) intrinsics (f, cx, cy) and (B..., 5) coefficients
+    (k1, k2, k3, p1, p2) -> (B..., 2) distorted pixels.  The skew term s (y'/z') of the reference's model is kept
+    with s = 0, so a non-finite y'/z' propagates as it does there."""
+    x, y, z = points[..., 0], points[..., 1], points[..., 2]
+    z = torch.where(z == 0, z + 1e-8, z)
+    f, cx, cy = intrinsics[..., 0], intrinsics[..., 1], intrinsics[..., 2]
+    k1, k2, k3, p1, p2 = coefficients.unbind(-1)
+    u = f * (x / z) + torch.zeros_like(f) * (y / z)
+    v = f * (y / z)
+    r2 = u * u + v * v
+    uv = u * v
+    radial = 1.0 + k1 * r2 + k2 * r2 * r2 + k3 * r2 * r2 * r2
+    ud = u * radial + 2.0 * p1 * uv + p2 * (r2 + 2 * u * u) + cx
+    vd = v * radial + 2.0 * p2 * uv + p1 * (r2 + 2 * v * v) + cy
+    return torch.stack([ud, vd], dim=-1)
+
+
+def _unpacked_points(parameters: torch.Tensor, num_views: int, num_points: int, distortion: bool):
+    from ..camera_model import unpack_calibration_parameters
+
+    base = parameters[..., :-5] if distortion else parameters
+    cam = unpack_calibration_parameters(base, num_views, num_points)
+    points = get_camera_relative_points(world_points=cam.world_points, camera_translations=cam.camera_translations,
+                                        camera_rotations=cam.camera_rotations)
+    return cam, points
+
+
+def reprojection_objective(parameters: torch.Tensor, observations: torch.Tensor, visibility: torch.Tensor,
+                           num_views: int, num_points: int, distortion: bool = False) -> torch.Tensor:
+    """E(x) = sum_{m,n} vis ||pi_m(X_n) - obs||^2 for (B..., P) parameters, (B..., M, N, 2) observations and
+    (B..., M, N) visibility: the squared objective the fused kernels evaluate, as torch ops."""
+    cam, points = _unpacked_points(parameters, num_views, num_points, distortion)
+    if distortion:
+        lead = parameters.shape[:-1]
+        uv = project_points_brown_conrady(points, cam.intrinsics, parameters[..., -5:].reshape(lead + (1, 1, 5)))
+    else:
+        uv = project_points_basic_pinhole(points, cam.intrinsics)
+    sq = (uv - observations).square().sum(dim=-1)
+    return (sq * visibility.to(sq.dtype)).sum(dim=(-1, -2))
+
+
+def ray_angle_objective(parameters: torch.Tensor, observations: torch.Tensor, visibility: torch.Tensor,
+                        num_views: int, num_points: int) -> torch.Tensor:
+    """sum_{m,n} vis * angle(ray(obs), p_m(X_n)): CalibrationNetwork's error (calibration_network.py:58-67)."""
+    cam, points = _unpacked_points(parameters, num_views, num_points, False)
+    rays = pixel_coordinates_to_homogeneous(observations, cam.intrinsics)
+    return (projective_plane_angle_distance(rays, points) * visibility.to(points.dtype)).sum(dim=(-1, -2))
