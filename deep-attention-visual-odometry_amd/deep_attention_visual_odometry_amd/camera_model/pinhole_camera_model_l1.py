@@ -18,8 +18,9 @@ returned detached; with ``enable_grad_gradients=False`` the gradient is differen
 world and camera-relative points held constant, as the reference's detaches do -- on a full
 evaluation only: its partial recompute of masked estimates (``:223-270``) detaches nothing, and
 neither does this one.  Gradients
-into ``true_projected_points`` are not provided: if it requires grad under grad mode,
-evaluation raises.
+into ``true_projected_points`` (r06) follow the reference's error: -scale sgn((u - t) vis) vis per pixel
+coordinate, formed from the reference's own torch expressions for u, v (``_target_term``); its hand-written
+gradient depends on them only through sign(), so not at all.
 """
 from typing import Optional
 
@@ -159,10 +160,6 @@ class PinholeCameraModelL1(IOptimisableFunction):
         inputs = (self._focal_length, self._cx, self._cy, self._translation, self._orientation.lie_vector,
                   self._world_points)
         differentiable = torch.is_grad_enabled() and any(t.requires_grad for t in inputs)
-        if torch.is_grad_enabled() and self._true_projected_points.requires_grad:
-            raise NotImplementedError(
-                "gradients into PinholeCameraModelL1's true_projected_points are not implemented on the GPU path; "
-                "detach them (the parameters may require grad)")
         dt = self._focal_length.dtype
         for t in inputs[1:] + (self._true_projected_points,):
             dt = torch.promote_types(dt, t.dtype)  # the dtype the reference's expressions produce
@@ -193,9 +190,30 @@ class PinholeCameraModelL1(IOptimisableFunction):
             err, grad = torch.ops.dava.l1_camera_evaluate(focal.detach(), cx.detach(), cy.detach(), trans.detach(),
                                                           lie.detach(), world.detach(), *fixed[:6],
                                                           bool(want_error), bool(want_gradient))
+        if want_error and torch.is_grad_enabled() and self._true_projected_points.requires_grad:
+            err = err + self._target_term(dt)
         err = err if want_error else None
         grad = grad if want_gradient else None
         return err, grad
+
+    def _target_term(self, dt: torch.dtype) -> torch.Tensor:
+        """A zero-valued (B, E) term whose gradient w.r.t. true_projected_points is the reference error's
+        (``:139-150``): d/dt sum scale |(u - t) vis| = -scale sgn((u - t) vis) vis (torch.abs backward, 0 at 0).
+        u, v come from the reference's own torch expressions (``_get_u`` / ``_get_v``, ``:467-496``); the error's
+        value stays the kernel's.  (The hand-written gradient depends on t only through sign(), whose derivative
+        is 0, as in the reference.)"""
+        t = self._true_projected_points.to(dt)
+        with torch.no_grad():
+            rel = self._get_camera_relative_points().to(dt)
+            f = self._focal_length.to(dt).reshape(self.batch_size, self.num_estimates, 1, 1)
+            u = f * rel[..., 0] / rel[..., 2] + self._cx.to(dt).reshape(f.shape)
+            v = f * rel[..., 1] / rel[..., 2] + self._cy.to(dt).reshape(f.shape)
+            vis = self._visibility_mask.to(dt)[:, None, :, :]
+            scale = self._error_scale.to(dt)
+            su = scale * torch.sign((u - t[:, None, :, :, 0]) * vis) * vis
+            sv = scale * torch.sign((v - t[:, None, :, :, 1]) * vis) * vis
+        term = -(su * t[:, None, :, :, 0] + sv * t[:, None, :, :, 1]).sum(dim=(-2, -1))
+        return term - term.detach()
 
     def get_error(self) -> torch.Tensor:
         """Total L1 reprojection error per estimate, (B, E) (``:132-190``)."""

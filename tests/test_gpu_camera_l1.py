@@ -324,12 +324,28 @@ def test_autograd_through_the_model_float32(device):
         assert _rel(a, b) < 1e-4, k
 
 
-def test_autograd_into_the_target_is_refused_loudly(device):
-    g = np.load(os.path.join(GOLDEN, "camera_l1.npz"))
-    t = {k: torch.tensor(g[f"default_f64_{k}"]) for k in FIELDS}
-    t["true"] = t["true"].requires_grad_(True)
-    with pytest.raises(NotImplementedError):
-        _model(device, t).get_error()
+@pytest.mark.parametrize("case", ["mg20", "behind"])
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+def test_autograd_into_the_target_matches_oracle(device, case, dtype):
+    """Gradients into true_projected_points (the reference's error is differentiable in them,
+    pinhole_camera_model_l1.py:139-150): d sum(we * error)/d true against the oracle's autograd, together with
+    the parameters' gradients; the error's value is unchanged by the target term."""
+    m, n, kw = AUTOGRAD_CASES[case]
+    t = _random_tensors(m, n, dtype=dtype)
+    true = t["true"].clone().to(device).requires_grad_(True)
+    model = _model(device, dict(t, true=true), **kw)
+    err = model.get_error()
+    plain = _model(device, t, **kw).get_error()
+    assert torch.equal(err.detach(), plain)
+    we = torch.randn(err.shape, generator=torch.Generator().manual_seed(2), dtype=torch.float64).to(device, dtype)
+    (g_true,) = torch.autograd.grad((err * we).sum(), true)
+    parts = {k: t[k].double() for k in PARAMS}
+    true_ref = t["true"].double().clone().requires_grad_(True)
+    zkw = {k: v for k, v in kw.items() if k != "max_gradient"}
+    e_ref = camera_l1.l1_error(*[parts[k] for k in PARAMS], true_ref, t["vis"], **zkw)
+    (g_ref,) = torch.autograd.grad((e_ref * we.double().cpu()).sum(), true_ref)
+    assert g_true.dtype == dtype
+    assert _rel(g_true, g_ref) < (1e-12 if dtype == torch.float64 else 1e-6), _rel(g_true, g_ref)
 
 
 def test_no_grad_evaluation_of_a_differentiable_model_is_detached(device):

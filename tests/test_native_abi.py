@@ -176,16 +176,20 @@ def test_adjoint_shapes(lib):
     assert lib.dava_ba_solve_tape_bytes(sc, cfg_dense) == 0
 
 
-def test_product_refuses_cpu_tensors():
+def test_fused_kernels_refuse_cpu_tensors():
+    """The fused solve and evaluation are GPU kernels: handed CPU tensors they raise, they never run elsewhere.
+    (BFGSSolver with a fused objective on CPU tensors takes the generic loop and the objective's torch form by
+    design, tests/test_cpu_solver.py -- not these kernels.)"""
     import torch
 
-    from deep_attention_visual_odometry_amd import BFGSSolver, ReprojectionError
+    from deep_attention_visual_odometry_amd import native_ops
 
     obs = torch.zeros(1, 2, 4, 2)
     vis = torch.ones(1, 2, 4, dtype=torch.bool)
-    fn = ReprojectionError(obs, vis, 2, 4)
     with pytest.raises(RuntimeError, match="ROCm device"):
-        BFGSSolver().eval()(torch.zeros(1, 3 + 12 + 6), fn)
+        native_ops.ba_solve(torch.zeros(1, 3 + 12 + 6), obs, vis, 2, 4, False)
+    with pytest.raises(RuntimeError, match="ROCm device"):
+        native_ops.ba_evaluate(torch.zeros(1, 3 + 12 + 6), obs, vis, 2, 4, False)
 
 
 def test_unpack_matches_reference_layout():
