@@ -386,12 +386,18 @@ __device__ __forceinline__ void dense_sweep(const Layout& L, int Pld, float* __r
 // (the rank-2 terms U_e the history stands for, compact_products), and continues with dense_sweep.  The
 // iteration cap alone never pays for the dense matrix: with the reference's stopping rules problems stop
 // long before 1025 iterations, in the compact phase.  Same mapping as dense_sweep (lane = float4 column
-// group, the wave's share of the groups), so every thread later reads back only what it wrote here;
-// kFoldRows rows per pass in registers, every history entry streamed once per pass.  Entries e < lcap
-// are the LDS-resident ones (LH: S row then W row).  The fold is a sum in entry order, not the
-// reference's sequence of rank-2 updates: the same matrix up to rounding, as COMPACT itself.
+// group, the wave's share of the groups), kFoldRows rows per pass in registers, every history entry streamed
+// once per pass.  Entries e < lcap are the LDS-resident ones (LH: S row then W row).  The fold is a sum in
+// entry order, not the reference's sequence of rank-2 updates: the same matrix up to rounding, as COMPACT
+// itself.  Its cost is P / kFoldRows passes over the whole history (at 8 rows: 157 GB per C5 problem, 34 of
+// the 41 s of a K = 1,100 C5 solve, profiles/r06h_hybrid_fold_k1100.jsonl).  One column per lane and 32 rows
+// (4x fewer bytes, the same 32 accumulators) was slower: its 64 row values per entry are wave-uniform
+// vector loads (C3 8.2 -> 14.3 s, C5 41.4 -> 67.7 s, profiles/r06i_fold_column_lanes_rejected.log).
 constexpr int kHybrid = 2;  // kernel MODE (internal; callers ask for DAVA_HESSIAN_COMPACT)
-constexpr int kFoldRows = 8;
+#ifndef DAVA_FOLD_ROWS
+#define DAVA_FOLD_ROWS 8
+#endif
+constexpr int kFoldRows = DAVA_FOLD_ROWS;
 template <int NW>
 __device__ void fold_history(int P, int Pv, int Pld, int nh, const float* __restrict__ S, const float* __restrict__ W,
                              const float* LH, int lcap, const float* hrho, const float* hc, float gamma0,

@@ -8,7 +8,9 @@
 #   configs: tools/measure_configs.sh on the in-tree build
 #   generic: the generic-loop GPU tests, the closure entry (compact vs dense) and tools/closure_profile.py
 #   hybrid : tools/hybrid_fold.sh (K = 1,100 fixed: the fold at iteration 1,025 against DENSE, C3 and C5)
-# usage: tools/session_r06.sh lean|gvlean|configs|generic|hybrid|diag ...
+#   defaults: the reference's defaults (cap 1,000, stopping rules) at C2, C3, C5
+#   profiles: tools/profile.sh (kernel trace, FETCH_SIZE, WRITE_SIZE) at C3, C2, C5
+# usage: tools/session_r06.sh lean|gvlean|configs|generic|hybrid|defaults|profiles|diag ...
 set -uo pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$R"
@@ -35,10 +37,64 @@ for s in "$@"; do
       echo "== closure profile"
       timeout -k 10 300 python3 tools/closure_profile.py > gpurun_out/closure_profile.log 2>&1 || { tail -5 gpurun_out/closure_profile.log; exit 1; }
       head -1 gpurun_out/closure_profile.log ;;
+    l1)
+      echo "== legacy L1 model GPU tests"
+      timeout -k 10 300 python3 -u -m pytest tests/test_gpu_camera_l1.py -m gpu -x -q --timeout 120 --timeout-method thread \
+        > gpurun_out/s6_l1_tests.log 2>&1; rc=$?; tail -2 gpurun_out/s6_l1_tests.log; [ $rc -eq 0 ] || exit 1 ;;
+    fold)
+      echo "== fold: bitwise r05 vs new at K = 1,100 (every problem folds at iteration 1,025)"
+      B=deep-attention-visual-odometry_amd/build
+      LIB=deep-attention-visual-odometry_amd/deep_attention_visual_odometry_amd/_lib/libdava_ba.so
+      for c in "--batch 64 --views 2 --points 128 --no-distortion" "--batch 64" "--batch 16 --views 16 --points 4096 --no-distortion"; do
+        timeout -k 10 300 python3 tools/lib_compare.py $B/var_r05/libdava_ba.so $LIB --seed 20254015 --k 1100 $c 2>&1 \
+          | grep -v amdgpu.ids | head -4 || exit 1
+      done
+      echo "== fold timing"
+      tools/hybrid_fold.sh > gpurun_out/hybrid_fold_new.jsonl || exit 1
+      cat gpurun_out/hybrid_fold_new.jsonl
+      echo "== hybrid GPU tests"
+      timeout -k 10 300 python3 -u -m pytest tests/test_gpu_hybrid.py -m gpu -x -q --timeout 200 --timeout-method thread \
+        > gpurun_out/s6_hybrid_tests.log 2>&1; rc=$?; tail -2 gpurun_out/s6_hybrid_tests.log; [ $rc -eq 0 ] || exit 1 ;;
+    foldab)
+      B=deep-attention-visual-odometry_amd/build
+      LIB=deep-attention-visual-odometry_amd/deep_attention_visual_odometry_amd/_lib/libdava_ba.so
+      echo "== fold rows: bitwise 8 vs 16 / 32 at K = 1,100"
+      for v in fold16 fold32; do
+        timeout -k 10 300 python3 tools/lib_compare.py $LIB $B/var_$v/libdava_ba.so --seed 20254015 --k 1100 --batch 64 2>&1 \
+          | grep -v amdgpu.ids | head -2 || exit 1
+      done
+      echo "== fold rows: timing (K = 1,100 fixed, compact = hybrid)"
+      for cfg in "C3:" "C5:--batch 256 --views 16 --points 4096 --no-distortion"; do
+        tag=${cfg%%:*}; args=${cfg#*:}
+        for v in rows8 fold16 fold32; do
+          e=""; [ $v != rows8 ] && e="DAVA_DEBUG_OVERRIDES=1 DAVA_LIB=$B/var_$v/libdava_ba.so"
+          out=$(env $e timeout -k 10 400 python3 bench.py --iterations 1100 --cpu-sample 0 --parity-envelope 0 \
+                --no-converged-parity --no-live-counters --sustain-seconds 0 --steps 1 --warmup 0 $args 2>&1 | tail -1) \
+            || { echo "$tag $v failed"; exit 1; }
+          echo "$tag $v $(echo "$out" | python3 -c 'import sys, json; d = json.loads(sys.stdin.read()); print(d["value"], d["ms_per_step"])')"
+        done
+      done ;;
+    defab)
+      tools/ab.sh -r 2 -c "C2def:--batch 1024 --views 2 --points 128 --no-distortion --iterations 1000 --error-threshold 1e-4 --minimum-step 1e-8 --no-converged-parity" \
+        -c "C3def:--iterations 1000 --error-threshold 1e-4 --minimum-step 1e-8 --no-converged-parity" \
+        "r05:DAVA_LIB=@BUILD@/var_r05/libdava_ba.so" "new:" 2>&1 | cut -c1-200 || exit 1 ;;
     hybrid)
       echo "== hybrid fold"
       tools/hybrid_fold.sh > gpurun_out/hybrid_fold.jsonl || exit 1
       cat gpurun_out/hybrid_fold.jsonl ;;
+    defaults)
+      echo "== reference defaults (cap 1,000, stopping rules 1e-4 / 1e-8)"
+      for cfg in "C2:--batch 1024 --views 2 --points 128 --no-distortion" "C3:" "C5:--batch 256 --views 16 --points 4096 --no-distortion"; do
+        tag=${cfg%%:*}; args=${cfg#*:}
+        timeout -k 10 300 python3 bench.py --iterations 1000 --error-threshold 1e-4 --minimum-step 1e-8 --cpu-sample 0 \
+          --no-converged-parity --no-live-counters --sustain-seconds 0 --steps 2 --warmup 1 $args > gpurun_out/def_$tag.log 2>&1 \
+          || { tail -5 gpurun_out/def_$tag.log; exit 1; }
+        echo "{\"tag\": \"${tag}_defaults\", \"line\": $(tail -1 gpurun_out/def_$tag.log)}" >> gpurun_out/defaults.jsonl
+        tail -1 gpurun_out/def_$tag.log | cut -c1-160
+      done ;;
+    profiles)
+      tools/gpu_run.sh profile=r06_c3 "profile_cfg=r06_c2:--batch 1024 --views 2 --points 128 --no-distortion" \
+        profile_c5=r06_c5 || exit 1 ;;
     diag)
       echo "== eval_bitwise"
       timeout -k 10 300 python3 tools/eval_bitwise.py 2>&1 | grep -v amdgpu.ids || exit 1
