@@ -151,7 +151,7 @@ __device__ __forceinline__ void ray_unit_backward(S r, S inv_n, const S (&u)[3],
 }
 
 template <bool GRAD, bool SLOPE, typename S>
-__device__ __forceinline__ void ray_angle_pair(const RayAngle<S>& ra, const float* ob, uint8_t visible, S p0,
+__device__ __forceinline__ void ray_angle_pair(const RayAngle<S>& ra, const S (&ob)[2], uint8_t visible, S p0,
                                                S p1, S p2, S dp0, S dp1, S dp2, S& e,
                                                S& sl, S (&gin)[8], S& G0, S& G1, S& G2, S& go0, S& go1) {
   const float wgt = visible ? 1.0f : 0.0f;
@@ -222,7 +222,7 @@ template <bool GRAD, bool SLOPE, bool TRIAL, bool DOT = false, bool CHECK = fals
 __device__ __forceinline__ bool ba_eval(const Layout& L, const S* x, const S* d, float alpha, const float* obs,
                                         const uint8_t* vis, S* grad, S* views, S* vpart, float* scratch, int& buf,
                                         S& E_out, S& slope_out, S* obs_grad = nullptr,
-                                        float* obs_tangent_acc = nullptr) {
+                                        float* obs_tangent_acc = nullptr, const float* obs_dir = nullptr) {
   constexpr int BLOCK = kWave * NW;  // threads in the workgroup
   static_assert(!DOT || (GRAD && !SLOPE), "DOT derives the slope from the reverse-mode gradient");
   static_assert(!CHECK || TRIAL, "CHECK needs a trial point");
@@ -420,7 +420,15 @@ __device__ __forceinline__ bool ba_eval(const Layout& L, const S* x, const S* d,
     // and stored back to `grad` by the caller below -- the same additions in the same order)
     auto pair = [&](int n, const S X0, const S X1, const S X2, const S dX0, const S dX1, const S dX2, S& q0, S& q1,
                     S& q2) {
-      const float ob[2] = {obs[2 * (m * N + n)], obs[2 * (m * N + n) + 1]};
+      // the pair's observation; for dual numbers with an observation direction (second derivatives in the
+      // observations, ba_second_order) it carries that tangent
+      S ob[2] = {obs[2 * (m * N + n)], obs[2 * (m * N + n) + 1]};
+      if constexpr (!std::is_same<S, float>::value) {
+        if (obs_dir) {
+          ob[0] = S(obs[2 * (m * N + n)], obs_dir[2 * (m * N + n)]);
+          ob[1] = S(obs[2 * (m * N + n) + 1], obs_dir[2 * (m * N + n) + 1]);
+        }
+      }
       const uint8_t visible = vis[m * N + n];
       const S a0 = X0 * inv_s, a1 = X1 * inv_s, a2 = X2 * inv_s;  // X~ = X / s
       S da0 = 0.f, da1 = 0.f, da2 = 0.f;

@@ -3,7 +3,9 @@
 // For each problem: E, g = dE/dx, H v (v a direction per problem), dE/dobs and
 // d(dE/dobs)/dx . v -- one launch, one workgroup per problem, the SAME objective
 // code as the solver (ba_objective.hpp) instantiated with Dual scalars and x
-// seeded with tangent v.  This is the node that lets the caller differentiate
+// seeded with tangent v.  With an observation direction u as well (r06), the
+// observations carry tangent u: the outputs become H v + (d2E/dx dobs) u and
+// (d2E/dobs dx) v + (d2E/dobs2) u -- differentiating dE/dobs again.  This is the node that lets the caller differentiate
 // THROUGH a solve whose error function is a fused objective: autograd's double
 // backward of the reference's closure (bfgs_solver.py:133-135, create_graph)
 // becomes g's VJP = H v (+ the mixed observation term).
@@ -14,7 +16,7 @@ namespace dava {
 struct SecondArgs {
   Layout L;
   int Pv;
-  const float *obs, *x, *v;
+  const float *obs, *x, *v, *obs_v;
   const uint8_t* vis;
   float *err, *grad, *hv, *obs_grad, *obs_hv;
 };
@@ -63,7 +65,8 @@ __global__ __launch_bounds__(kBlock) void ba_second_order_kernel(SecondArgs a) {
   int buf = 0;
   Dual E(0.0f), unused(0.0f);
   ba_eval<true, false, false, false, false, RES, Dual>(L, x, nullptr, 0.0f, obs, vis, g, views, vpart, scratch, buf,
-                                                       E, unused, obsd);
+                                                       E, unused, obsd, nullptr,
+                                                       a.obs_v ? a.obs_v + (size_t)b * 2 * MN : nullptr);
   if (tid == 0 && a.err) a.err[b] = E.v;
   for (int i = tid; i < P; i += kBlock) {
     if (a.grad) a.grad[(size_t)b * P + i] = g[i].v;
@@ -104,6 +107,13 @@ using namespace dava;
 extern "C" int dava_ba_second_order(const DavaScene* scene, const float* x, const float* direction,
                                     float* error_out, float* grad_out, float* hv_out, float* obs_grad_out,
                                     float* obs_hv_out, void* stream) {
+  return dava_ba_second_order_obs(scene, x, direction, nullptr, error_out, grad_out, hv_out, obs_grad_out, obs_hv_out,
+                                  stream);
+}
+
+extern "C" int dava_ba_second_order_obs(const DavaScene* scene, const float* x, const float* direction,
+                                        const float* obs_direction, float* error_out, float* grad_out, float* hv_out,
+                                        float* obs_grad_out, float* obs_hv_out, void* stream) {
   const int st = second_check(scene);
   if (st != DAVA_OK) return st;
   if (scene->batch == 0) return DAVA_OK;
@@ -118,6 +128,7 @@ extern "C" int dava_ba_second_order(const DavaScene* scene, const float* x, cons
   a.vis = scene->visibility;
   a.x = x;
   a.v = direction;
+  a.obs_v = obs_direction;
   a.err = error_out;
   a.grad = grad_out;
   a.hv = hv_out;

@@ -389,15 +389,22 @@ __device__ __forceinline__ void dense_sweep(const Layout& L, int Pld, float* __r
 // group, the wave's share of the groups), kFoldRows rows per pass in registers, every history entry streamed
 // once per pass.  Entries e < lcap are the LDS-resident ones (LH: S row then W row).  The fold is a sum in
 // entry order, not the reference's sequence of rank-2 updates: the same matrix up to rounding, as COMPACT
-// itself.  Its cost is P / kFoldRows passes over the whole history (at 8 rows: 157 GB per C5 problem, 34 of
-// the 41 s of a K = 1,100 C5 solve, profiles/r06h_hybrid_fold_k1100.jsonl).  One column per lane and 32 rows
-// (4x fewer bytes, the same 32 accumulators) was slower: its 64 row values per entry are wave-uniform
-// vector loads (C3 8.2 -> 14.3 s, C5 41.4 -> 67.7 s, profiles/r06i_fold_column_lanes_rejected.log).
+// itself.  Its cost is P / kFoldRows passes over the whole history, and per entry and pass 2 kFoldRows row
+// values every lane needs: loaded once, coalesced, by 2 kFoldRows lanes and broadcast through SGPRs
+// (v_readlane; kFoldReadlane) rather than as wave-uniform vector loads.  K = 1,100 fixed (every problem folds;
+// interleaved, bitwise equal, profiles/r06j_fold_rows_readlane_ab.log): 8 rows with uniform loads (r05) C3
+// 8.33 s, C5 41.9 s (the fold ~34 s of it); 16 / 32 rows with uniform loads C5 19.3 / 47.0 s; readlane 16 / 32
+// rows C5 17.3 / **14.4 s**, C3 7.64 / **7.17 s**.  (One column per lane, 32 rows, uniform loads: C5 67.7 s,
+// profiles/r06i_fold_column_lanes_rejected.log.)
 constexpr int kHybrid = 2;  // kernel MODE (internal; callers ask for DAVA_HESSIAN_COMPACT)
 #ifndef DAVA_FOLD_ROWS
-#define DAVA_FOLD_ROWS 8
+#define DAVA_FOLD_ROWS 32
 #endif
 constexpr int kFoldRows = DAVA_FOLD_ROWS;
+#ifndef DAVA_FOLD_READLANE
+#define DAVA_FOLD_READLANE 1
+#endif
+constexpr bool kFoldReadlane = DAVA_FOLD_READLANE != 0;
 template <int NW>
 __device__ void fold_history(int P, int Pv, int Pld, int nh, const float* __restrict__ S, const float* __restrict__ W,
                              const float* LH, int lcap, const float* hrho, const float* hc, float gamma0,
@@ -432,12 +439,30 @@ __device__ void fold_history(int P, int Pv, int Pld, int nh, const float* __rest
             v[q] = rho * sj[q];
           }
         }
+        if constexpr (kFoldReadlane) {
+          // the pass's 2R row values in one coalesced load (lane r: s_e[i0 + r], lane R + r: w_e[i0 + r]), then
+          // broadcast to every lane through SGPRs (v_readlane) instead of 2R wave-uniform vector loads
+          static_assert(2 * R <= kWave, "one row value per lane");
+          float rv = 0.f;
+          if (lane < 2 * R) {
+            const int rr = lane < R ? lane : lane - R;
+            rv = (lane < R ? sr : wr)[min(i0 + rr, P - 1)];
+          }
 #pragma unroll
-        for (int r = 0; r < R; ++r) {
-          const int i = min(i0 + r, P - 1);  // (rows past P are computed and dropped)
-          const float si = sr[i], wi = wr[i];
+          for (int r = 0; r < R; ++r) {
+            const float si = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(rv), r));
+            const float wi = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(rv), R + r));
 #pragma unroll
-          for (int q = 0; q < 4; ++q) h[r][q] += si * u[q] - wi * v[q];
+            for (int q = 0; q < 4; ++q) h[r][q] += si * u[q] - wi * v[q];
+          }
+        } else {
+#pragma unroll
+          for (int r = 0; r < R; ++r) {
+            const int i = min(i0 + r, P - 1);  // (rows past P are computed and dropped)
+            const float si = sr[i], wi = wr[i];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) h[r][q] += si * u[q] - wi * v[q];
+          }
         }
       }
       if (act)

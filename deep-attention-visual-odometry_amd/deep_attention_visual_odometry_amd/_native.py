@@ -96,6 +96,7 @@ SIGNATURES = {
                                      _vp, ctypes.c_size_t, _vp]),
     "dava_ba_evaluate": (ctypes.c_int, [ctypes.POINTER(DavaScene), _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "dava_ba_second_order": (ctypes.c_int, [ctypes.POINTER(DavaScene)] + [_vp] * 8),
+    "dava_ba_second_order_obs": (ctypes.c_int, [ctypes.POINTER(DavaScene)] + [_vp] * 9),
     "dava_ba_solve_tape_bytes": (ctypes.c_size_t, [ctypes.POINTER(DavaScene), ctypes.POINTER(DavaSolverConfig)]),
     "dava_ba_solve_record": (ctypes.c_int, [ctypes.POINTER(DavaScene), ctypes.POINTER(DavaSolverConfig), _vp, _vp,
                                             _vp, _vp, _vp, ctypes.c_size_t, _vp]),

@@ -177,14 +177,17 @@ def _(x, observations, visibility, num_views, num_points, distortion, direction,
 @torch.library.custom_op("dava::ba_second_order", mutates_args=(), device_types=_CUDA)
 def ba_second_order(x: Tensor, observations: Tensor, visibility: Tensor, num_views: int, num_points: int,
                     distortion: bool, direction: Optional[Tensor], residual: int, want_hv: bool,
-                    want_obs: bool) -> Tuple[Tensor, Tensor, Tensor, Tensor, Tensor]:
-    """``dava_ba_second_order``: (E, dE/dx, H v, dE/dobs, (d2E/dobs dx) v), forward-over-reverse.
-    direction None means v = 0.  Unrequested outputs are empty."""
+                    want_obs: bool, obs_direction: Optional[Tensor] = None) -> Tuple[Tensor, Tensor, Tensor, Tensor, Tensor]:
+    """``dava_ba_second_order_obs``: (E, dE/dx, H v + (d2E/dx dobs) u, dE/dobs, (d2E/dobs dx) v + (d2E/dobs2) u),
+    forward-over-reverse.  direction / obs_direction None mean v = 0 / u = 0.  Unrequested outputs are empty."""
     lib = N.load_library()
     _check_scene_tensors(x, observations, visibility, num_views, num_points, distortion)
     if direction is not None and (direction.shape != x.shape or direction.dtype != torch.float32
                                   or not direction.is_contiguous()):
         raise ValueError("direction must be a contiguous float32 tensor of the parameters' shape")
+    if obs_direction is not None and (obs_direction.shape != observations.shape or obs_direction.dtype != torch.float32
+                                      or not obs_direction.is_contiguous()):
+        raise ValueError("obs_direction must be a contiguous float32 tensor of the observations' shape")
     b = x.shape[0]
     err = torch.empty(b, device=x.device, dtype=torch.float32)
     grad = torch.empty_like(x)
@@ -193,15 +196,17 @@ def ba_second_order(x: Tensor, observations: Tensor, visibility: Tensor, num_vie
     obs_hv = torch.empty_like(observations) if (want_obs and want_hv) else _empty0(x)
     sc = scene_struct(observations, visibility, num_views, num_points, distortion, b, residual)
     with torch.cuda.device(x.device):
-        N.check(lib.dava_ba_second_order(sc, N.ptr(x), N.ptr(direction), N.ptr(err), N.ptr(grad),
-                                         N.ptr(hv) if want_hv else None, N.ptr(obs_grad) if want_obs else None,
-                                         N.ptr(obs_hv) if (want_obs and want_hv) else None, N.stream_of(x.device)),
-                "dava_ba_second_order")
+        N.check(lib.dava_ba_second_order_obs(sc, N.ptr(x), N.ptr(direction), N.ptr(obs_direction), N.ptr(err),
+                                             N.ptr(grad), N.ptr(hv) if want_hv else None,
+                                             N.ptr(obs_grad) if want_obs else None,
+                                             N.ptr(obs_hv) if (want_obs and want_hv) else None, N.stream_of(x.device)),
+                "dava_ba_second_order_obs")
     return err, grad, hv, obs_grad, obs_hv
 
 
 @ba_second_order.register_fake
-def _(x, observations, visibility, num_views, num_points, distortion, direction, residual, want_hv, want_obs):
+def _(x, observations, visibility, num_views, num_points, distortion, direction, residual, want_hv, want_obs,
+      obs_direction=None):
     b = x.shape[0]
     return (x.new_empty((b,)), torch.empty_like(x), torch.empty_like(x) if want_hv else x.new_empty((0,)),
             torch.empty_like(observations) if want_obs else x.new_empty((0,)),

@@ -97,15 +97,14 @@ class _NativeGradient(torch.autograd.Function):
     @staticmethod
     @torch.autograd.function.once_differentiable
     def backward(ctx, u, u_obs):
-        if u_obs is not None and bool((u_obs != 0).any()):
-            raise NotImplementedError("differentiating dE/dobs again (second derivatives in the observations) "
-                                      "is not implemented for the fused objectives")
-        if u is None:
+        # u_obs: a cotangent on dE/dobs (differentiating it again): the observations carry it as a tangent in
+        # the same forward-over-reverse launch (dava_ba_second_order_obs)
+        if u is None and u_obs is None:
             return None, None, None, None, None, None, None
         x, obs, vis = ctx.saved_tensors
         _, _, hv, _, obs_hv = native_ops.ba_second_order(x, obs, vis, *ctx.meta[:3], direction=u,
                                                           residual=ctx.meta[3],
-                                                          want_obs=ctx.needs_input_grad[1])
+                                                          want_obs=ctx.needs_input_grad[1], obs_direction=u_obs)
         return (hv if ctx.needs_input_grad[0] else None, obs_hv if ctx.needs_input_grad[1] else None,
                 None, None, None, None, None)
 

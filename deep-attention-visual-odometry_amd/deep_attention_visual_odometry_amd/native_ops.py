@@ -54,14 +54,17 @@ def ba_evaluate(x: torch.Tensor, observations: torch.Tensor, visibility: torch.T
 def ba_second_order(x: torch.Tensor, observations: torch.Tensor, visibility: torch.Tensor, num_views: int,
                     num_points: int, distortion: bool = False, direction: Optional[torch.Tensor] = None,
                     residual: int = N.DAVA_RESIDUAL_SQUARED_REPROJECTION, want_hv: bool = True,
-                    want_obs: bool = True):
-    """(E, dE/dx, H v, dE/dobs, (d2E/dobs dx) v) for a (B, P) fp32 batch (``torch.ops.dava.ba_second_order``).
-    ``direction`` None means v = 0 (then only E, dE/dx and dE/dobs are meaningful)."""
+                    want_obs: bool = True, obs_direction: Optional[torch.Tensor] = None):
+    """(E, dE/dx, H v + (d2E/dx dobs) u, dE/dobs, (d2E/dobs dx) v + (d2E/dobs2) u) for a (B, P) fp32 batch
+    (``torch.ops.dava.ba_second_order``).  ``direction`` / ``obs_direction`` None mean v = 0 / u = 0 (with both
+    None only E, dE/dx and dE/dobs are meaningful)."""
     x = _fp32_on_device(x, "x")
     obs, vis = _scene_inputs(x, observations, visibility)
+    if obs_direction is not None:
+        obs_direction = _c(obs_direction.detach().to(device=x.device, dtype=torch.float32)).reshape(obs.shape)
     err, grad, hv, obs_grad, obs_hv = torch.ops.dava.ba_second_order(
         x, obs, vis, num_views, num_points, bool(distortion), _opt(direction), int(residual), bool(want_hv),
-        bool(want_obs))
+        bool(want_obs), obs_direction)
     return (err, grad, hv if want_hv else None, obs_grad if want_obs else None,
             obs_hv if (want_obs and want_hv) else None)
 

@@ -205,6 +205,14 @@ int dava_ba_evaluate(const DavaScene* scene, const float* x, const float* direct
  * Shapes whose dual LDS image exceeds 160 KiB return DAVA_ERR_UNSUPPORTED.                 */
 int dava_ba_second_order(const DavaScene* scene, const float* x, const float* direction, float* error_out,
                          float* grad_out, float* hv_out, float* obs_grad_out, float* obs_hv_out, void* stream);
+/* The same with an observation direction u (B, M, N, 2) as well (NULL = 0; r06, additive to ABI 4): the
+ * observations carry tangent u, so
+ *   hv_out     = (d^2E/dx^2) v + (d^2E/dx dobs) u
+ *   obs_hv_out = (d^2E/dobs dx) v + (d^2E/dobs^2) u
+ * -- what differentiating dE/dobs again needs (PyTorch double backward of the fused objectives). */
+int dava_ba_second_order_obs(const DavaScene* scene, const float* x, const float* direction, const float* obs_direction,
+                             float* error_out, float* grad_out, float* hv_out, float* obs_grad_out, float* obs_hv_out,
+                             void* stream);
 
 /* ---- generic BFGS building blocks (drive an arbitrary error closure) ----
  * batch = number of problems (all leading dims flattened), n = P.          */

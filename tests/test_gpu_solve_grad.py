@@ -239,6 +239,61 @@ def test_gradient_through_a_fused_objective_solve_matches_reference(device, name
     assert _rel(obs.grad.cpu(), torch.tensor(g[name + "_obs_grad"])) < 1e-3
 
 
+def _second_oracle_obs(x, obs, vis, m, n, distortion, residual, v, u):
+    """H v + (d2E/dx dobs) u and (d2E/dobs dx) v + (d2E/dobs2) u by torch double backward through the oracle, fp64."""
+    x64 = x.double().clone().requires_grad_(True)
+    o64 = obs.double().clone().requires_grad_(True)
+    if residual == "ray":
+        e = objective.ray_angle_error(x64, o64, vis, m, n)
+    else:
+        e = objective.reprojection_error(x64, o64, vis, m, n, distortion)
+    g, og = torch.autograd.grad(e.sum(), (x64, o64), create_graph=True)
+    return torch.autograd.grad((g * v.double()).sum() + (og * u.double()).sum(), (x64, o64))
+
+
+@pytest.mark.parametrize("residual,distortion", [("sq", False), ("sq", True), ("ray", False)])
+def test_second_order_in_the_observations_matches_double_backward(device, residual, distortion):
+    """dava_ba_second_order_obs: the observations carry a tangent u as well as x a tangent v (r06; r05 raised
+    for any u != 0): H v + (d2E/dx dobs) u and (d2E/dobs dx) v + (d2E/dobs2) u against fp64 double backward of
+    the oracle, with v = 0 and with both."""
+    from deep_attention_visual_odometry_amd import make_scenes, native_ops
+    from deep_attention_visual_odometry_amd._native import DAVA_RESIDUAL_RAY_ANGLE, DAVA_RESIDUAL_SQUARED_REPROJECTION
+
+    m, n = (4, 64) if distortion else (2, 64)
+    s = make_scenes(3, m, n, distortion=distortion, seed=77, drop=0.0 if distortion else 0.1,
+                    ray_angle=residual == "ray")
+    x, obs, vis = torch.tensor(s.initial), torch.tensor(s.observations), torch.tensor(s.visibility)
+    gen = torch.Generator().manual_seed(4)
+    u = torch.randn(obs.shape, generator=gen) * 1e-2
+    res = DAVA_RESIDUAL_RAY_ANGLE if residual == "ray" else DAVA_RESIDUAL_SQUARED_REPROJECTION
+    for v in (torch.zeros_like(x), torch.randn(x.shape, generator=gen) * x.abs().clamp(min=0.1) * 1e-2):
+        _, _, hv, _, ohv = native_ops.ba_second_order(x.to(device), obs.to(device), vis.to(device), m, n, distortion,
+                                                      direction=v.to(device), residual=res,
+                                                      obs_direction=u.to(device))
+        hv_ref, ohv_ref = _second_oracle_obs(x, obs, vis, m, n, distortion, residual, v, u)
+        for b in range(3):
+            assert _rel(hv[b].cpu(), hv_ref[b]) < 1e-3, ("hv", b)
+            assert _rel(ohv[b].cpu(), ohv_ref[b]) < 1e-3, ("obs hv", b)
+
+
+def test_fused_objective_dE_dobs_is_differentiable_again(device):
+    """torch double backward through ReprojectionError's dE/dobs (the reference's closure is plain autograd,
+    differentiable to any order in true_projected_points, calibration_network.py:58-67): d/d(x, obs) of
+    sum(w * dE/dobs) against the oracle's."""
+    from deep_attention_visual_odometry_amd import ReprojectionError, make_scenes
+
+    s = make_scenes(2, 2, 32, seed=9, drop=0.1)
+    x, obs, vis = torch.tensor(s.initial), torch.tensor(s.observations), torch.tensor(s.visibility)
+    w = torch.randn(obs.shape, generator=torch.Generator().manual_seed(6))
+    xd = x.to(device).requires_grad_(True)
+    od = obs.to(device).requires_grad_(True)
+    e = ReprojectionError(od, vis.to(device), 2, 32)(xd, torch.ones(2, dtype=torch.bool, device=device))
+    (go,) = torch.autograd.grad(e.sum(), od, create_graph=True)
+    gx, gobs = torch.autograd.grad((go * w.to(device)).sum(), (xd, od))
+    hv_ref, ohv_ref = _second_oracle_obs(x, obs, vis, 2, 32, False, "sq", torch.zeros_like(x), w)
+    assert _rel(gx.cpu(), hv_ref) < 1e-3 and _rel(gobs.cpu(), ohv_ref) < 1e-3
+
+
 def test_fused_objective_first_order_obs_gradient(device):
     """d E / d obs of the fused objective (first order, no solve)."""
     from deep_attention_visual_odometry_amd import ReprojectionError, make_scenes

@@ -59,14 +59,14 @@ for s in "$@"; do
       B=deep-attention-visual-odometry_amd/build
       LIB=deep-attention-visual-odometry_amd/deep_attention_visual_odometry_amd/_lib/libdava_ba.so
       echo "== fold rows: bitwise 8 vs 16 / 32 at K = 1,100"
-      for v in fold16 fold32; do
+      for v in fold16 fold32 rl16 rl32; do
         timeout -k 10 300 python3 tools/lib_compare.py $LIB $B/var_$v/libdava_ba.so --seed 20254015 --k 1100 --batch 64 2>&1 \
           | grep -v amdgpu.ids | head -2 || exit 1
       done
       echo "== fold rows: timing (K = 1,100 fixed, compact = hybrid)"
       for cfg in "C3:" "C5:--batch 256 --views 16 --points 4096 --no-distortion"; do
         tag=${cfg%%:*}; args=${cfg#*:}
-        for v in rows8 fold16 fold32; do
+        for v in rows8 fold16 fold32 rl16 rl32; do
           e=""; [ $v != rows8 ] && e="DAVA_DEBUG_OVERRIDES=1 DAVA_LIB=$B/var_$v/libdava_ba.so"
           out=$(env $e timeout -k 10 400 python3 bench.py --iterations 1100 --cpu-sample 0 --parity-envelope 0 \
                 --no-converged-parity --no-live-counters --sustain-seconds 0 --steps 1 --warmup 0 $args 2>&1 | tail -1) \
@@ -78,6 +78,18 @@ for s in "$@"; do
       tools/ab.sh -r 2 -c "C2def:--batch 1024 --views 2 --points 128 --no-distortion --iterations 1000 --error-threshold 1e-4 --minimum-step 1e-8 --no-converged-parity" \
         -c "C3def:--iterations 1000 --error-threshold 1e-4 --minimum-step 1e-8 --no-converged-parity" \
         "r05:DAVA_LIB=@BUILD@/var_r05/libdava_ba.so" "new:" 2>&1 | cut -c1-200 || exit 1 ;;
+    bitwise)
+      B=deep-attention-visual-odometry_amd/build
+      LIB=deep-attention-visual-odometry_amd/deep_attention_visual_odometry_amd/_lib/libdava_ba.so
+      for c in "--batch 1024 --views 2 --points 128 --no-distortion" "--batch 2048" \
+               "--batch 1024 --views 2 --points 128 --no-distortion --residual ray_angle" \
+               "--batch 64 --views 16 --points 4096 --no-distortion"; do
+        echo "== bitwise r05 vs new: $c"
+        timeout -k 10 300 python3 tools/lib_compare.py $B/var_r05/libdava_ba.so $LIB --seed 20254015 $c 2>&1 \
+          | grep -v amdgpu.ids | head -3 || exit 1
+      done ;;
+    final)
+      tools/gpu_run.sh tests smoke bench || exit 1 ;;
     hybrid)
       echo "== hybrid fold"
       tools/hybrid_fold.sh > gpurun_out/hybrid_fold.jsonl || exit 1
