@@ -394,11 +394,14 @@ __device__ __forceinline__ void dense_sweep(const Layout& L, int Pld, float* __r
 // (v_readlane; kFoldReadlane) rather than as wave-uniform vector loads.  K = 1,100 fixed (every problem folds;
 // interleaved, bitwise equal, profiles/r06j_fold_rows_readlane_ab.log): 8 rows with uniform loads (r05) C3
 // 8.33 s, C5 41.9 s (the fold ~34 s of it); 16 / 32 rows with uniform loads C5 19.3 / 47.0 s; readlane 16 / 32
-// rows C5 17.3 / **14.4 s**, C3 7.64 / **7.17 s**.  (One column per lane, 32 rows, uniform loads: C5 67.7 s,
+// rows C5 **17.3** / 14.4 s, C3 **7.64** / 7.17 s.  16 rows: at 32 (128 accumulators) the LDS-mode ray-angle
+// hybrid kernel -- already at 256 VGPRs with ~300 SGPRs spilled -- returned wrong results
+// (test_hybrid_switch_ray_angle_matches_oracle, rel 0.83; 16 and 8 rows pass,
+// profiles/r06l_fold_variants_hybrid_ray_test.log).  (One column per lane, 32 rows, uniform loads: C5 67.7 s,
 // profiles/r06i_fold_column_lanes_rejected.log.)
 constexpr int kHybrid = 2;  // kernel MODE (internal; callers ask for DAVA_HESSIAN_COMPACT)
 #ifndef DAVA_FOLD_ROWS
-#define DAVA_FOLD_ROWS 32
+#define DAVA_FOLD_ROWS 16
 #endif
 constexpr int kFoldRows = DAVA_FOLD_ROWS;
 #ifndef DAVA_FOLD_READLANE

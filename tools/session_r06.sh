@@ -90,6 +90,14 @@ for s in "$@"; do
       done ;;
     final)
       tools/gpu_run.sh tests smoke bench || exit 1 ;;
+    foldvar)
+      B=deep-attention-visual-odometry_amd/build
+      for v in intree rl16 shfl32 rows8; do
+        e=""; [ $v != intree ] && e="DAVA_DEBUG_OVERRIDES=1 DAVA_LIB=$B/var_$v/libdava_ba.so"
+        echo "== $v"
+        env $e timeout -k 10 300 python3 -u -m pytest tests/test_gpu_hybrid.py -m gpu -q --timeout 200 --timeout-method thread \
+          -k "ray_angle" 2>&1 | grep -E "passed|failed|Error" | tail -3
+      done ;;
     hybrid)
       echo "== hybrid fold"
       tools/hybrid_fold.sh > gpurun_out/hybrid_fold.jsonl || exit 1
