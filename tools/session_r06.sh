@@ -98,6 +98,16 @@ for s in "$@"; do
         env $e timeout -k 10 300 python3 -u -m pytest tests/test_gpu_hybrid.py -m gpu -q --timeout 200 --timeout-method thread \
           -k "ray_angle" 2>&1 | grep -E "passed|failed|Error" | tail -3
       done ;;
+    c2scan)
+      echo "== C2 / C2 ray-angle batch scan"
+      for bsz in 256 1024 4096 8192; do
+        for res in reprojection ray_angle; do
+          out=$(timeout -k 10 300 python3 bench.py --batch $bsz --views 2 --points 128 --no-distortion --residual $res \
+                --cpu-sample 0 --parity-envelope 0 --no-live-counters --sustain-seconds 0 --steps 3 --warmup 1 2>&1 | tail -1) \
+            || { echo "c2scan $bsz $res failed"; exit 1; }
+          echo "B=$bsz $res $(echo "$out" | python3 -c 'import sys, json; d = json.loads(sys.stdin.read()); r = d["roofline"]; g = d["diagnostics"]["per_problem"]; print(d["value"], d["ms_per_step"], "frac", r["frac"], "evals p50/p99/max", [g["evaluations"][k] for k in ("p50", "p99", "max")])')"
+        done
+      done ;;
     hybrid)
       echo "== hybrid fold"
       tools/hybrid_fold.sh > gpurun_out/hybrid_fold.jsonl || exit 1
