@@ -150,17 +150,23 @@ def wolfe_line_search(
 
 
 def ulp_jitter(t: torch.Tensor, gen: torch.Generator) -> torch.Tensor:
-    """t with every element moved by -1, 0 or +1 ulp (uniformly at random from `gen`)."""
+    """t with every finite element moved by -1, 0 or +1 ulp (uniformly at random from `gen`); inf and NaN stay
+    (a reordered sum that overflows still overflows: nextafter(inf, -inf) would make it finite)."""
     sign = torch.randint(0, 3, t.shape, generator=gen) - 1
     up = torch.nextafter(t, torch.full_like(t, float("inf")))
     down = torch.nextafter(t, torch.full_like(t, -float("inf")))
-    return torch.where(sign > 0, up, torch.where(sign < 0, down, t))
+    moved = torch.where(sign > 0, up, torch.where(sign < 0, down, t))
+    return torch.where(torch.isfinite(t), moved, t)
 
 
 def _jittered_closure(closure, gen: torch.Generator):
     def fn(x: torch.Tensor, mask: torch.Tensor) -> torch.Tensor:
         out = closure(x, mask)
-        return out + (ulp_jitter(out.detach(), gen) - out.detach())  # the value moves, its gradient does not
+        d = out.detach()
+        # the value moves, its gradient does not; an overflowed value stays as it is (inf - inf would be NaN,
+        # and the NaN-blind Wolfe tests branch differently on NaN than on inf)
+        delta = torch.where(torch.isfinite(d), ulp_jitter(d, gen) - d, torch.zeros_like(d))
+        return out + delta
     return fn
 
 
