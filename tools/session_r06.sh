@@ -108,6 +108,20 @@ for s in "$@"; do
           echo "B=$bsz $res $(echo "$out" | python3 -c 'import sys, json; d = json.loads(sys.stdin.read()); r = d["roofline"]; g = d["diagnostics"]["per_problem"]; print(d["value"], d["ms_per_step"], "frac", r["frac"], "evals p50/p99/max", [g["evaluations"][k] for k in ("p50", "p99", "max")])')"
         done
       done ;;
+    c2waves)
+      tools/ab.sh -r 2 -c "C2:--batch 1024 --views 2 --points 128 --no-distortion" \
+        -c "C2b256:--batch 256 --views 2 --points 128 --no-distortion" \
+        "w2:" "w4:DAVA_SOLVE_WAVES=4" 2>&1 | cut -c1-200 || exit 1 ;;
+    extra)
+      echo "== C3 at B = 65,536 on one GPU (the 8-GPU global batch)"
+      timeout -k 10 400 python3 bench.py --batch 65536 --cpu-sample 0 --parity-envelope 0 --no-converged-parity \
+        --no-live-counters --sustain-seconds 0 --steps 2 --warmup 1 > gpurun_out/extra_b65536.log 2>&1 || exit 1
+      tail -1 gpurun_out/extra_b65536.log | cut -c1-200
+      echo "== C3 solve + gradient at the reference's default cap (B = 4096, stopping rules)"
+      timeout -k 10 400 python3 bench.py --batch 4096 --differentiate --iterations 1000 --error-threshold 1e-4 \
+        --minimum-step 1e-8 --cpu-sample 0 --no-live-counters --sustain-seconds 0 --steps 2 --warmup 1 \
+        > gpurun_out/extra_grad_defaults.log 2>&1 || exit 1
+      tail -1 gpurun_out/extra_grad_defaults.log | cut -c1-200 ;;
     hybrid)
       echo "== hybrid fold"
       tools/hybrid_fold.sh > gpurun_out/hybrid_fold.jsonl || exit 1
